@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mray/s on the final random-spheres scene, 3840x2160 @ 500 spp,
+depth 50 (BASELINE.json `metric`, config 3), on 1..8 MI355X of one node.
+
+One step = one full frame: every rank renders its interleaved row bands
+ with the HIP kernel through the C ABI (rt_render_async on torch's
+current stream, device-resident frame tile), then rank 0 gathers the tiles
+with one RCCL gather over xGMI.  Strong scaling: the frame is fixed, N GPUs
+split it.  `value` = closest-hit queries (ray segments) of all ranks per
+second of the max-over-ranks wall time / 1e6.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Extra objects on the JSON line:
+  roofline     fp32 VALU roofline of the render kernel (algorithmic flops =
+               segments x spheres x 17 per launch / average launch time from
+               HIP events on the launch stream; peak 157.3 TFLOP/s)
+  cpu_baseline the reference's own src/cpu (oracle/_ref, built from
+               /root/reference sources) on 1 host core over a bounded sample,
+               falling back to the oracle's fp64 restatement (kind "port")
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "ray-tracing-in-one-weekend_amd")
+sys.path.insert(0, PKG)
+
+PEAK_FP32_TFLOPS = 157.3      # MI355X vector fp32 (MI355X_MICROARCH.md, chip table)
+FLOPS_PER_TEST = 17           # algorithmic flops per ray-sphere test
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--spp", type=int, default=500)
+    ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--half-extent", type=int, default=11, help="11: 486 spheres; 50: 10k spheres")
+    ap.add_argument("--row-block", type=int, default=8)
+    ap.add_argument("--cpu-spp", type=int, default=30, help="spp of the bounded CPU sample (400x225)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--out", default="", help="write the gathered frame as PPM (P6 if .pgm/.p6)")
+    return ap.parse_args()
+
+
+def cpu_baseline(spp):
+    """Reference src/cpu (compiled from /root/reference by oracle/Makefile) on one
+    host core: 400x225 (C0 geometry) at `spp` samples, depth 50."""
+    sample = f"final scene 400x225 @ {spp} spp, depth 50, single thread"
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if os.path.exists(harness):
+        r = subprocess.run([harness, "render", "400", "16", "9", str(spp), "50", "final", "0"],
+                           stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, check=True, timeout=600)
+        st = json.loads(r.stderr.decode().strip().splitlines()[-1])
+        return {"value": round(st["segments"] / st["seconds"] / 1e6, 4), "unit": "Mray/s",
+                "cores": 1, "kind": "reference", "seconds": round(st["seconds"], 3),
+                "sample": sample + " (reference src/cpu, g++ -O2)"}
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    t = time.perf_counter()
+    _, segs = oracle_lib.reference_render(400, 16.0 / 9.0, spp)
+    dt = time.perf_counter() - t
+    return {"value": round(segs / dt / 1e6, 4), "unit": "Mray/s", "cores": 1, "kind": "port",
+            "seconds": round(dt, 3), "sample": sample + " (oracle fp64 restatement)"}
+
+
+def load_traffic(workload):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            sys.exit("for --gpus N > 1 launch with torch.distributed.run --nproc-per-node N")
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import rtow
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=dev)
+
+    W, H, spp = a.width, a.height, a.spp
+    workload = f"final random-spheres scene {W}x{H} @ {spp}spp depth {a.depth}"
+    scene = rtow.final_scene(a.half_extent)
+    cam = rtow.camera_cpu(aspect=W / H)
+    ctx = rtow.Context(local_rank)
+    ctx.upload(scene)
+    params = rtow.make_params(W, H, spp, max_depth=a.depth, rank=rank, world=world,
+                              row_block=a.row_block)
+    params.flags |= rtow.RT_FLAG_KEEP_COUNTERS
+    tile = torch.zeros((params.local_rows, W, 3), dtype=torch.float32, device=dev)
+    gather_list = [torch.empty_like(tile) for _ in range(world)] if (world > 1 and rank == 0) else None
+    stream = torch.cuda.current_stream(dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local_rank])
+
+    def step(i, events=None):
+        params.seed = i
+        if events is not None:
+            events[0].record(stream)
+        ctx.render_async(cam, params, tile.data_ptr(), stream.cuda_stream)
+        if events is not None:
+            events[1].record(stream)
+        if world > 1:
+            dist.gather(tile, gather_list, dst=0)
+
+    for i in range(a.warmup):
+        step(1000 + i)
+    torch.cuda.synchronize(dev)
+    ctx.reset_stats(stream.cuda_stream)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(a.steps)]
+
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        step(i, evs[i])
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    st = ctx.collect_stats()
+    kernel_ms = [e0.elapsed_time(e1) for e0, e1 in evs]
+    local = torch.tensor([float(st.segments), float(st.samples), float(st.wave_steps)],
+                         dtype=torch.float64, device=dev)
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(local, op=dist.ReduceOp.SUM)
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    segments, samples, wave_steps = local.tolist()
+    elapsed = float(t_max.item())
+
+    if rank == 0:
+        # assemble the last frame on rank 0 (outside the timed region) and sanity-check it
+        if world > 1:
+            tiles = torch.stack(gather_list).cpu().numpy()
+        else:
+            tiles = tile.cpu().numpy()[None]
+        frame = np.zeros((H, W, 3), np.float32)
+        for r in range(world):
+            p = rtow.make_params(W, H, spp, rank=r, world=world, row_block=a.row_block)
+            rows = rtow.local_to_global_rows(p)
+            keep = rows < H
+            frame[rows[keep]] = tiles[r][keep]
+        assert np.isfinite(frame).all() and frame.max() <= spp + 1e-3
+        if a.out:
+            rtow.write_ppm(a.out, rtow.tonemap(frame, spp), binary=a.out.endswith((".p6", ".pnm")))
+
+        seg_per_launch_rank0 = st.segments / a.steps
+        k_avg_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+        achieved = seg_per_launch_rank0 * scene.n * FLOPS_PER_TEST / k_avg_s / 1e12
+        value = segments / elapsed / 1e6
+        out = {
+            "metric": "Mray/s (ray segments = closest-hit queries per second), final random-spheres "
+                      "scene 3840x2160 @ 500spp depth 50",
+            "value": round(value, 2),
+            "unit": "Mray/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic: final random-spheres scene (g++-order mt19937 seed 5489, "
+                    f"{scene.n} spheres), src/cpu camera",
+            "config": {"workload": workload, "width": W, "height": H, "spp": spp,
+                       "max_depth": a.depth, "spheres": scene.n,
+                       "parallelism": f"row-interleaved bands of {a.row_block} rows x {world} GPU"
+                                      + (" + RCCL gather" if world > 1 else "")},
+            "ms_per_frame": round(elapsed / a.steps * 1e3, 3),
+            "msamples_per_s": round(samples / elapsed / 1e6, 2),
+            "segments_per_frame": int(segments / a.steps),
+            "lane_efficiency": round(segments / (64.0 * wave_steps), 4) if wave_steps else None,
+            "kernel_ms_avg_rank0": round(k_avg_s * 1e3, 3),
+            "roofline": {"bound": "valu", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+                         "traffic": load_traffic(workload),
+                         "note": "fp32 VALU-bound (no MFMA): 17 flop per ray-sphere test x "
+                                 "spheres x segments per launch / HIP-event kernel time"},
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(a.cpu_spp)
+            except Exception as e:  # the GPU number stands on its own
+                out["cpu_baseline"] = {"value": None, "error": repr(e)[:200]}
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,207 @@
+/*
+ * rt.h -- C ABI of the MI355X-native render path (librtow.so).
+ *
+ * The reference (kouei/ray-tracing-in-one-weekend) has no library or FFI; its
+ * "interface" is (1) the process surface of cpu_ray_tracer / gpu_ray_tracer and
+ * (2) the in-process kernel contract
+ *     render(color *frame_buffer, camera *cam, hittable *world, seed)
+ * (src/gpu/camera.h:169-195).  This header replaces (2) with plain pointers and
+ * sizes; (1) is kept by the rt_* CLIs built on top of it.  Each entry point
+ * names the reference code it stands in for.
+ *
+ * Conventions
+ *  - Every function returns 0 (RT_OK) or a negative rt_status; no exit() inside.
+ *  - Host arrays passed in are copied; the caller keeps ownership.
+ *  - A context is bound to one HIP device and must be used from one host
+ *    thread at a time.  Multi-GPU = one context per device (one process per
+ *    GPU in bench.py, RCCL gather of the frame tiles).
+ *  - Frame buffers are W * rows * 3 fp32, row-major, row 0 = TOP image row,
+ *    holding UNNORMALISED per-pixel sums over spp samples (the reference's
+ *    frame_buffer contract, src/gpu/camera.h:194).
+ */
+#ifndef RTOW_RT_H
+#define RTOW_RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+typedef enum {
+  RT_OK = 0,
+  RT_ERR_INVALID = -1,    /* bad argument (null pointer, bad size, bad enum) */
+  RT_ERR_HIP = -2,        /* a HIP runtime call failed (see rt_last_hip_error) */
+  RT_ERR_NOMEM = -3,      /* host or device allocation failed */
+  RT_ERR_NO_DEVICE = -4,  /* no HIP device with that ordinal */
+  RT_ERR_CAPACITY = -5,   /* caller buffer too small */
+  RT_ERR_NO_SCENE = -6,   /* rt_render before rt_scene_upload */
+  RT_ERR_IO = -7          /* write to fd failed */
+} rt_status;
+
+/* material kinds -- src/cpu/material.h:15-88 (lambertian, metal, dielectric) */
+typedef enum { RT_LAMBERTIAN = 0, RT_METAL = 1, RT_DIELECTRIC = 2 } rt_material_kind;
+
+/* camera models -- src/cpu/camera.h (default, parity) / src/gpu/camera.h */
+typedef enum { RT_CAMERA_CPU = 0, RT_CAMERA_GPU = 1 } rt_camera_model;
+
+/* render flags (semantic switches between the two reference variants,
+ * SURVEY Appendix A).  0 = src/cpu semantics. */
+enum {
+  RT_FLAG_OPEN_INTERVAL = 1u << 0,     /* interval::surrounds, src/gpu/sphere.h:31-36 */
+  RT_FLAG_METAL_UNIT_VECTOR = 1u << 1, /* fuzz*random_unit_vector, src/gpu/material.h:51-52 */
+  RT_FLAG_GPU_SEMANTICS = RT_FLAG_OPEN_INTERVAL | RT_FLAG_METAL_UNIT_VECTOR,
+  /* bookkeeping, not semantics: do not zero the context's segment counters
+   * before this launch (rt_collect_stats then reports the sum over launches
+   * since the last rt_reset_stats) */
+  RT_FLAG_KEEP_COUNTERS = 1u << 8
+};
+
+/* Scene as structure-of-arrays; n spheres.  Replaces the device-heap
+ * hittable_list of virtual sphere objects (src/gpu/hittable_list.h:49-65,
+ * src/gpu/sphere.h) and the shared_ptr list of src/cpu/hittable_list.h. */
+typedef struct {
+  uint32_t n;
+  const float *cx, *cy, *cz, *radius; /* n each; radius may be negative */
+  const uint32_t *mat_kind;           /* n, rt_material_kind */
+  const float *albedo_rgb;            /* 3n (ignored for dielectric) */
+  const float *mat_param;             /* n: metal fuzz (already min(f,1)) | ior */
+} rt_scene_view;
+
+/* Caller-owned output buffers for the host scene builders. */
+typedef struct {
+  uint32_t capacity; /* entries available in every array below */
+  uint32_t n;        /* written: number of spheres */
+  float *cx, *cy, *cz, *radius;
+  uint32_t *mat_kind;
+  float *albedo_rgb; /* 3 * capacity */
+  float *mat_param;
+} rt_scene_buf;
+
+/* Camera, already reduced to what get_ray needs (fp32, computed in fp64).
+ *  CPU model (src/cpu/camera.h:28-34):
+ *    s=(i+x)/(W-1), t=(j+y)/(H-1) with j counted from the bottom row,
+ *    target = corner + s*horiz + t*vert        (corner = lower_left_corner)
+ *  GPU model (src/gpu/camera.h:153-167):
+ *    target = corner + (i+x-0.5)*horiz + (row+y-0.5)*vert
+ *                                               (corner = pixel00_loc,
+ *                                                horiz/vert = pixel_delta_u/v)
+ *  origin = eye + dx*lens_u + dy*lens_v, (dx,dy) uniform in the unit disk,
+ *  applied only when has_lens != 0. */
+typedef struct {
+  int32_t model; /* rt_camera_model */
+  int32_t has_lens;
+  float eye[3];
+  float corner[3];
+  float horiz[3];
+  float vert[3];
+  float lens_u[3]; /* lens_radius * u  (gpu: defocus_disk_u) */
+  float lens_v[3]; /* lens_radius * v  (gpu: defocus_disk_v) */
+} rt_camera;
+
+/* Render parameters.  Rows are partitioned across ranks in interleaved bands
+ * (SURVEY 8e): local row r of this rank is global row
+ *     ((r / row_block) * band_stride + band_offset) * row_block + r % row_block
+ * Rows >= height are padding and come out as zeros.  A single-GPU render is
+ * row_block = height (or any), band_stride = 1, band_offset = 0,
+ * local_rows = height. */
+typedef struct {
+  int32_t width, height;
+  int32_t spp, max_depth;
+  uint64_t seed;
+  int32_t row_block;
+  int32_t band_stride;
+  int32_t band_offset;
+  int32_t local_rows;
+  uint32_t flags;
+  uint32_t reserved;
+} rt_params;
+
+typedef struct {
+  uint64_t segments;     /* closest-hit queries (= hittable_list::hit calls) */
+  uint64_t samples;      /* primary samples rendered (width*rows*spp) */
+  uint64_t sphere_tests; /* segments * spheres scanned (brute force) */
+  uint64_t wave_steps;   /* sum over waves of bounce iterations (lane-efficiency denominator / 64) */
+  double kernel_ms;      /* hipEvent time of the render kernel (0 if async) */
+} rt_stats;
+
+typedef struct rt_context rt_context;
+
+/* ---- misc ---- */
+int rt_abi_version(void);
+const char *rt_strerror(int status);
+int rt_last_hip_error(void); /* hipError_t of the last RT_ERR_HIP on this thread */
+int rt_device_count(int *count);
+
+/* ---- host scene / camera builders (run once per frame, fp64 host code) ---- */
+
+/* Final random-spheres scene, random_scene() src/cpu/main.cc:32-76.
+ * Draws from std::mt19937 (default seed 5489) through
+ * uniform_real_distribution<double> in the order g++ 11 evaluates the
+ * reference's argument lists (z-jitter before x-jitter, vec3 components
+ * z,y,x -- SURVEY 8a-1), then casts to fp32.  half_extent = 11 gives the
+ * reference's 22x22 grid (486 spheres); 50 gives the 10 000-sphere stress
+ * scene of BASELINE config 5.  If rng_next is non-null it receives the next
+ * random_double() after the scene (the reference renders from that point). */
+int rt_scene_final(int half_extent, rt_scene_buf *out, double *rng_next);
+
+/* Five-sphere book scene (archive-gpu/image22/main.cu:23-38; hollow glass
+ * sphere of negative radius). */
+int rt_scene_five(rt_scene_buf *out);
+
+/* camera::camera, src/cpu/camera.h:8-26 */
+int rt_camera_cpu(const double lookfrom[3], const double lookat[3],
+                  const double vup[3], double vfov_deg, double aspect,
+                  double aperture, double focus_dist, rt_camera *out);
+
+/* new_camera, src/gpu/camera.h:53-110 (image size decides the viewport) */
+int rt_camera_gpu(const double lookfrom[3], const double lookat[3],
+                  const double vup[3], double vfov_deg, int width, int height,
+                  double defocus_angle_deg, double focus_dist, rt_camera *out);
+
+/* ---- device context ---- */
+int rt_context_create(int device_ordinal, rt_context **out);
+void rt_context_destroy(rt_context *ctx);
+
+/* Copies the scene to the device (geometry padded for the scan kernel).
+ * Replaces new_world<<<1,1>>> (src/gpu/main.cu:18-75). */
+int rt_scene_upload(rt_context *ctx, const rt_scene_view *scene);
+
+/* Enqueue the render kernel on `stream` (a hipStream_t, NULL = the context's
+ * own stream) writing params->width * params->local_rows * 3 floats to the
+ * DEVICE pointer accum_rgb.  Replaces render<<<>>> (src/gpu/camera.h:169-195).
+ * Does not synchronise.  Segment counters are read by rt_collect_stats after
+ * the stream has completed. */
+int rt_render_async(rt_context *ctx, const rt_camera *cam, const rt_params *params,
+                    float *accum_rgb, void *stream);
+
+/* Synchronous convenience: render into a context-owned device buffer, time the
+ * kernel with hipEvents, copy the sums to HOST memory host_rgb
+ * (width*local_rows*3 floats) and fill stats (may be NULL). */
+int rt_render(rt_context *ctx, const rt_camera *cam, const rt_params *params,
+              float *host_rgb, rt_stats *stats);
+
+/* Stats of the last rt_render_async (or, with RT_FLAG_KEEP_COUNTERS, of all
+ * launches since rt_reset_stats); call after the stream has completed. */
+int rt_collect_stats(rt_context *ctx, rt_stats *stats);
+
+/* Zero the segment counters (enqueued on `stream`, NULL = context stream). */
+int rt_reset_stats(rt_context *ctx, void *stream);
+
+/* ---- output (write_color src/cpu/color.h:8-23, output_image
+ *      src/gpu/camera.h:197-210) ---- */
+
+/* int(256 * clamp(sqrt(sum/spp), 0, 0.999)) per channel, fp64 like src/cpu. */
+int rt_tonemap_u8(const float *sums_rgb, size_t n_pixels, int spp, uint8_t *out_rgb);
+
+/* "P3\nW H\n255\n" + one "r g b\n" line per pixel (binary P6 if binary!=0).
+ * Rows are written top to bottom, as both references do. */
+int rt_write_ppm(int fd, const uint8_t *rgb, int width, int height, int binary);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RTOW_RT_H */

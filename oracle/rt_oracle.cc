@@ -1,0 +1,633 @@
+// oracle/rt_oracle.cc -- TEST INFRASTRUCTURE ONLY.  CPU restatement of the
+// reference's render path, used by tests/ (and bench.py's cpu_baseline leg)
+// as the CHECKER.  Never linked into, or called by, the product
+// (librtow.so / the CLIs); the product fails loudly without its HIP build.
+//
+// Two modes, both written from the reference's semantics (not copied):
+//
+//  * reference mode (rto_reference_render): single-threaded fp64 restatement
+//    of src/cpu -- one std::mt19937 (seed 5489) + uniform_real_distribution
+//    <double> stream shared by scene construction and rendering
+//    (src/cpu/rtweekend.h:27-31), rejection sampling, recursive ray_color,
+//    closed hit interval, g++ argument evaluation order.  Pinned: byte-
+//    identical PPM to the reference binary built from /root/reference by
+//    oracle/Makefile (tests/golden/ref_c0_*.ppm.gz, SHA-256 736ab8c6...).
+//
+//  * kernel mode (rto_kernel_render): fp32 restatement of the algorithm the
+//    HIP kernel runs (DESIGN.md "Kernel algorithm"): normalised directions,
+//    expanded quadratic, pcg4d counter RNG, closed-form sampling.  Written
+//    independently of ray-tracing-in-one-weekend_amd/csrc/rt_render.hip from
+//    the same specification; with -ffp-contract=off and explicit fmaf it is
+//    the bit-exact per-pixel parity partner of the GPU kernel.
+//
+// Reference anchors are cited per function (paths under /root/reference).
+#include "rt_oracle.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <random>
+#include <thread>
+#include <vector>
+
+namespace {
+
+// =====================================================================
+// reference mode (fp64)
+// =====================================================================
+
+struct d3 {
+  double x, y, z;
+};
+inline d3 operator+(d3 a, d3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline d3 operator-(d3 a, d3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline d3 operator-(d3 a) { return {-a.x, -a.y, -a.z}; }
+inline d3 operator*(d3 a, d3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+inline d3 operator*(double t, d3 v) { return {t * v.x, t * v.y, t * v.z}; }  // vec3.h:83-85
+inline d3 operator/(d3 v, double t) { return (1 / t) * v; }                    // vec3.h:91
+inline double dot(d3 a, d3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline double len2(d3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+inline d3 cross(d3 u, d3 v) {
+  return {u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
+}
+inline d3 unit(d3 v) { return v / std::sqrt(len2(v)); }  // vec3.h:103
+
+// rtweekend.h:27-36
+struct rng64 {
+  std::mt19937 gen;
+  std::uniform_real_distribution<double> dist{0.0, 1.0};
+  double operator()() { return dist(gen); }
+  double operator()(double lo, double hi) { return lo + (hi - lo) * (*this)(); }
+};
+
+// vec3.h:105-112 random_in_unit_sphere; vec3::random(-1,1) draws z,y,x (g++)
+d3 in_unit_sphere(rng64 &r) {
+  while (true) {
+    d3 p;
+    p.z = r(-1, 1);
+    p.y = r(-1, 1);
+    p.x = r(-1, 1);
+    if (len2(p) >= 1) continue;
+    return p;
+  }
+}
+
+// vec3.h:133-140 random_in_unit_disk; vec3(rd(-1,1), rd(-1,1), 0): y drawn first
+d3 in_unit_disk(rng64 &r) {
+  while (true) {
+    d3 p;
+    p.z = 0;
+    p.y = r(-1, 1);
+    p.x = r(-1, 1);
+    if (len2(p) >= 1) continue;
+    return p;
+  }
+}
+
+struct dsphere {
+  d3 c;
+  double r;
+  int kind;
+  d3 albedo;
+  double param;
+};
+
+struct dhit {
+  d3 p, n;
+  double t;
+  bool front;
+  int obj;
+};
+
+// sphere.h:24-51
+bool sphere_hit(const dsphere &s, d3 o, d3 d, double tmin, double tmax, dhit &rec) {
+  d3 oc = o - s.c;
+  double a = len2(d);
+  double half_b = dot(oc, d);
+  double c = len2(oc) - s.r * s.r;
+  double disc = half_b * half_b - a * c;
+  if (disc < 0) return false;
+  double sq = std::sqrt(disc);
+  double root = (-half_b - sq) / a;
+  if (root < tmin || tmax < root) {
+    root = (-half_b + sq) / a;
+    if (root < tmin || tmax < root) return false;
+  }
+  rec.t = root;
+  rec.p = o + root * d;                   // ray.h at()
+  d3 outward = (rec.p - s.c) / s.r;
+  rec.front = dot(d, outward) < 0;        // hittable.h:16-19
+  rec.n = rec.front ? outward : -outward;
+  return true;
+}
+
+struct dworld {
+  std::vector<dsphere> s;
+  unsigned long long calls = 0;
+  // hittable_list.h:28-43
+  bool hit(d3 o, d3 d, double tmin, double tmax, dhit &rec) {
+    ++calls;
+    dhit tmp;
+    bool any = false;
+    double closest = tmax;
+    for (size_t i = 0; i < s.size(); ++i) {
+      if (sphere_hit(s[i], o, d, tmin, closest, tmp)) {
+        any = true;
+        closest = tmp.t;
+        rec = tmp;
+        rec.obj = (int)i;
+      }
+    }
+    return any;
+  }
+};
+
+d3 reflect(d3 v, d3 n) { return v - (2 * dot(v, n)) * n; }  // vec3.h:122
+
+d3 refract(d3 uv, d3 n, double eta) {  // vec3.h:126-131
+  double cos_theta = std::fmin(dot(-uv, n), 1.0);
+  d3 perp = eta * (uv + cos_theta * n);
+  d3 par = (-std::sqrt(std::fabs(1.0 - len2(perp)))) * n;
+  return perp + par;
+}
+
+double reflectance(double cosine, double ref_idx) {  // material.h:82-87
+  double r0 = (1 - ref_idx) / (1 + ref_idx);
+  r0 = r0 * r0;
+  return r0 + (1 - r0) * std::pow((1 - cosine), 5);
+}
+
+// material.h scatter functions; returns false when absorbed
+bool scatter(const dsphere &m, d3 din, const dhit &rec, rng64 &r, d3 &att, d3 &dout) {
+  if (m.kind == RT_LAMBERTIAN) {  // material.h:19-30
+    d3 dir = rec.n + unit(in_unit_sphere(r));
+    const double s = 1e-8;
+    if (std::fabs(dir.x) < s && std::fabs(dir.y) < s && std::fabs(dir.z) < s) dir = rec.n;
+    dout = dir;
+    att = m.albedo;
+    return true;
+  }
+  if (m.kind == RT_METAL) {  // material.h:40-46
+    d3 refl = reflect(unit(din), rec.n);
+    dout = refl + m.param * in_unit_sphere(r);
+    att = m.albedo;
+    return dot(dout, rec.n) > 0;
+  }
+  // dielectric, material.h:57-76
+  att = {1.0, 1.0, 1.0};
+  double ratio = rec.front ? (1.0 / m.param) : m.param;
+  d3 ud = unit(din);
+  double cos_t = std::fmin(dot(-ud, rec.n), 1.0);
+  double sin_t = std::sqrt(1.0 - cos_t * cos_t);
+  bool cannot = ratio * sin_t > 1.0;
+  if (cannot || reflectance(cos_t, ratio) > r())
+    dout = reflect(ud, rec.n);
+  else
+    dout = refract(ud, rec.n, ratio);
+  return true;
+}
+
+// main.cc:12-30 (recursive)
+d3 ray_color(d3 o, d3 d, dworld &w, rng64 &r, int depth) {
+  if (depth <= 0) return {0, 0, 0};
+  dhit rec;
+  if (w.hit(o, d, 0.001, INFINITY, rec)) {
+    d3 att, dir;
+    if (scatter(w.s[rec.obj], d, rec, r, att, dir)) return att * ray_color(rec.p, dir, w, r, depth - 1);
+    return {0, 0, 0};
+  }
+  d3 ud = unit(d);
+  double t = 0.5 * (ud.y + 1.0);
+  return (1.0 - t) * d3{1.0, 1.0, 1.0} + t * d3{0.5, 0.7, 1.0};
+}
+
+// main.cc:32-76 random_scene, g++ draw order
+void final_scene(rng64 &r, int half, std::vector<dsphere> &s) {
+  s.push_back({{0, -1000, 0}, 1000, RT_LAMBERTIAN, {0.5, 0.5, 0.5}, 0});
+  for (int a = -half; a < half; a++) {
+    for (int b = -half; b < half; b++) {
+      double choose = r();
+      d3 c;
+      c.y = 0.2;
+      c.z = b + 0.9 * r();
+      c.x = a + 0.9 * r();
+      if (std::sqrt(len2(c - d3{4, 0.2, 0})) > 0.9) {
+        if (choose < 0.8) {
+          d3 rhs, lhs;
+          rhs.z = r(); rhs.y = r(); rhs.x = r();
+          lhs.z = r(); lhs.y = r(); lhs.x = r();
+          s.push_back({c, 0.2, RT_LAMBERTIAN, lhs * rhs, 0});
+        } else if (choose < 0.95) {
+          d3 alb;
+          alb.z = r(0.5, 1); alb.y = r(0.5, 1); alb.x = r(0.5, 1);
+          double fuzz = r(0, 0.5);
+          s.push_back({c, 0.2, RT_METAL, alb, fuzz < 1 ? fuzz : 1});
+        } else {
+          s.push_back({c, 0.2, RT_DIELECTRIC, {1, 1, 1}, 1.5});
+        }
+      }
+    }
+  }
+  s.push_back({{0, 1, 0}, 1.0, RT_DIELECTRIC, {1, 1, 1}, 1.5});
+  s.push_back({{-4, 1, 0}, 1.0, RT_LAMBERTIAN, {0.4, 0.2, 0.1}, 0});
+  s.push_back({{4, 1, 0}, 1.0, RT_METAL, {0.7, 0.6, 0.5}, 0.0});
+}
+
+void five_scene(std::vector<dsphere> &s) {
+  s.push_back({{0.0, -100.5, -1.0}, 100.0, RT_LAMBERTIAN, {0.8, 0.8, 0.0}, 0});
+  s.push_back({{0.0, 0.0, -1.0}, 0.5, RT_LAMBERTIAN, {0.1, 0.2, 0.5}, 0});
+  s.push_back({{-1.0, 0.0, -1.0}, 0.5, RT_DIELECTRIC, {1, 1, 1}, 1.5});
+  s.push_back({{-1.0, 0.0, -1.0}, -0.4, RT_DIELECTRIC, {1, 1, 1}, 1.5});
+  s.push_back({{1.0, 0.0, -1.0}, 0.5, RT_METAL, {0.8, 0.6, 0.2}, 0.0});
+}
+
+inline uint8_t tonemap(double v, double scale) {  // color.h:8-23
+  double x = std::sqrt(scale * v);
+  if (x < 0.0) x = 0.0;
+  if (x > 0.999) x = 0.999;
+  return (uint8_t)(int)(256 * x);
+}
+
+// =====================================================================
+// kernel mode (fp32) -- the specification the HIP kernel implements
+// =====================================================================
+
+inline float fmaf_(float a, float b, float c) { return std::fmaf(a, b, c); }
+
+struct u4 {
+  uint32_t x, y, z, w;
+};
+
+// pcg4d, Jarzynski & Olano, JCGT 9(3) 2020
+u4 pcg4d(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  uint32_t x = a * 1664525u + 1013904223u;
+  uint32_t y = b * 1664525u + 1013904223u;
+  uint32_t z = c * 1664525u + 1013904223u;
+  uint32_t w = d * 1664525u + 1013904223u;
+  x += y * w;
+  y += z * x;
+  z += x * y;
+  w += y * z;
+  x ^= x >> 16;
+  y ^= y >> 16;
+  z ^= z >> 16;
+  w ^= w >> 16;
+  x += y * w;
+  y += z * x;
+  z += x * y;
+  w += y * z;
+  return {x, y, z, w};
+}
+
+inline float unif(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
+
+void sincos_turn(float u, float &s, float &c) {
+  float q4 = u * 4.0f;
+  float qf = std::floor(q4);
+  int q = (int)qf;
+  float x = (q4 - qf) * 1.57079632679489662f;
+  float x2 = x * x;
+  float sp = fmaf_(x2, -2.50521084e-08f, 2.75573192e-06f);
+  sp = fmaf_(x2, sp, -1.98412698e-04f);
+  sp = fmaf_(x2, sp, 8.33333333e-03f);
+  sp = fmaf_(x2, sp, -1.66666667e-01f);
+  sp = fmaf_(x2, sp, 1.0f);
+  float sn = x * sp;
+  float cp = fmaf_(x2, 2.08767570e-09f, -2.75573192e-07f);
+  cp = fmaf_(x2, cp, 2.48015873e-05f);
+  cp = fmaf_(x2, cp, -1.38888889e-03f);
+  cp = fmaf_(x2, cp, 4.16666667e-02f);
+  cp = fmaf_(x2, cp, -0.5f);
+  float cs = fmaf_(x2, cp, 1.0f);
+  float s0 = (q & 1) ? cs : sn;
+  float c0 = (q & 1) ? sn : cs;
+  s = (q & 2) ? -s0 : s0;
+  c = ((q + 1) & 2) ? -c0 : c0;
+}
+
+float cbrt01(float u) {
+  uint32_t i;
+  std::memcpy(&i, &u, 4);
+  i = i / 3u + 709921077u;
+  float y;
+  std::memcpy(&y, &i, 4);
+  for (int k = 0; k < 3; ++k) {
+    float y2 = y * y;
+    y = fmaf_(y, 0.666666687f, (u / y2) * 0.333333343f);
+  }
+  return u == 0.0f ? 0.0f : y;
+}
+
+void unit_vec(float u1, float u2, float &x, float &y, float &z) {
+  z = fmaf_(-2.0f, u1, 1.0f);
+  float r = std::sqrt(std::fmax(fmaf_(-z, z, 1.0f), 0.0f));
+  float s, c;
+  sincos_turn(u2, s, c);
+  x = r * c;
+  y = r * s;
+}
+
+inline float dot3(float ax, float ay, float az, float bx, float by, float bz) {
+  return fmaf_(az, bz, fmaf_(ay, by, ax * bx));
+}
+
+void normalize3(float &x, float &y, float &z) {
+  float inv = 1.0f / std::sqrt(dot3(x, y, z, x, y, z));
+  x *= inv;
+  y *= inv;
+  z *= inv;
+}
+
+struct kscene {
+  std::vector<float> cx, cy, cz, ks, inv_r, ar, ag, ab, param;
+  std::vector<uint32_t> kind;
+};
+
+struct kctx {
+  const kscene *sc;
+  const rt_camera *cam;
+  const rt_params *p;
+  uint32_t seed32;
+  bool open, metal_unit;
+};
+
+void camera_ray(const kctx &k, uint32_t pix, int col, int grow, uint32_t sample, float o[3],
+                float d[3]) {
+  const rt_camera &c = *k.cam;
+  u4 r = pcg4d(pix, sample, 0u, k.seed32);
+  float u1 = unif(r.x), u2 = unif(r.y);
+  float fs, ft;
+  if (c.model == RT_CAMERA_CPU) {
+    int j = k.p->height - 1 - grow;
+    fs = ((float)col + u1) / (float)(k.p->width - 1);
+    ft = ((float)j + u2) / (float)(k.p->height - 1);
+  } else {
+    fs = (float)col + (u1 - 0.5f);
+    ft = (float)grow + (u2 - 0.5f);
+  }
+  float t[3];
+  for (int a = 0; a < 3; ++a) t[a] = fmaf_(ft, c.vert[a], fmaf_(fs, c.horiz[a], c.corner[a]));
+  for (int a = 0; a < 3; ++a) o[a] = c.eye[a];
+  if (c.has_lens) {
+    float rr = std::sqrt(unif(r.z));
+    float s, cc;
+    sincos_turn(unif(r.w), s, cc);
+    float ddx = rr * cc, ddy = rr * s;
+    for (int a = 0; a < 3; ++a) o[a] = fmaf_(ddy, c.lens_v[a], fmaf_(ddx, c.lens_u[a], o[a]));
+  }
+  for (int a = 0; a < 3; ++a) d[a] = t[a] - o[a];
+  normalize3(d[0], d[1], d[2]);
+}
+
+inline bool in_range(bool open, float t, float tmin, float tmax) {
+  return open ? (t > tmin && t < tmax) : (t >= tmin && t <= tmax);
+}
+
+// one pixel, all samples; returns number of closest-hit queries
+unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) {
+  const kscene &sc = *k.sc;
+  const uint32_t pix = (uint32_t)grow * (uint32_t)k.p->width + (uint32_t)col;
+  const size_t n = sc.cx.size();
+  unsigned long long segs = 0;
+  acc[0] = acc[1] = acc[2] = 0.0f;
+  if (k.p->max_depth <= 0) return 0;  // ray_color(.., 0) is black, no hit test
+  for (uint32_t sample = 0; sample < (uint32_t)k.p->spp; ++sample) {
+    float o[3], d[3];
+    camera_ray(k, pix, col, grow, sample, o, d);
+    float th[3] = {1.0f, 1.0f, 1.0f};
+    for (int depth = 0;;) {
+      ++segs;
+      // closest hit: expanded quadratic with |d| = 1
+      const float nk1 = -dot3(o[0], o[1], o[2], d[0], d[1], d[2]);
+      const float o2 = dot3(o[0], o[1], o[2], o[0], o[1], o[2]);
+      const float ox2 = -2.0f * o[0], oy2 = -2.0f * o[1], oz2 = -2.0f * o[2];
+      float tmax = INFINITY;
+      long best = -1;
+      for (size_t i = 0; i < n; ++i) {
+        const float h = fmaf_(sc.cz[i], d[2], fmaf_(sc.cy[i], d[1], fmaf_(sc.cx[i], d[0], nk1)));
+        const float g = fmaf_(sc.cz[i], oz2, fmaf_(sc.cy[i], oy2, fmaf_(sc.cx[i], ox2, o2)));
+        const float e = fmaf_(h, h, -g);
+        if (e >= sc.ks[i]) {
+          const float sq = std::sqrt(e - sc.ks[i]);
+          const float t0 = h - sq, t1 = h + sq;
+          const bool ok0 = in_range(k.open, t0, 0.001f, tmax);
+          const bool ok1 = in_range(k.open, t1, 0.001f, tmax);
+          if (ok0 || ok1) {
+            tmax = ok0 ? t0 : t1;
+            best = (long)i;
+          }
+        }
+      }
+      if (best < 0) {  // sky, main.cc:27-29
+        const float a = 0.5f * (d[1] + 1.0f);
+        const float s0 = 1.0f - a;
+        acc[0] = fmaf_(th[0], fmaf_(a, 0.5f, s0), acc[0]);
+        acc[1] = fmaf_(th[1], fmaf_(a, 0.7f, s0), acc[1]);
+        acc[2] = fmaf_(th[2], s0 + a, acc[2]);
+        break;
+      }
+      const size_t b = (size_t)best;
+      float p[3], nn[3];
+      for (int a = 0; a < 3; ++a) p[a] = fmaf_(tmax, d[a], o[a]);
+      nn[0] = (p[0] - sc.cx[b]) * sc.inv_r[b];
+      nn[1] = (p[1] - sc.cy[b]) * sc.inv_r[b];
+      nn[2] = (p[2] - sc.cz[b]) * sc.inv_r[b];
+      const bool front = dot3(d[0], d[1], d[2], nn[0], nn[1], nn[2]) < 0.0f;
+      if (!front)
+        for (int a = 0; a < 3; ++a) nn[a] = -nn[a];
+      const u4 r = pcg4d(pix, sample, (uint32_t)(depth + 1), k.seed32);
+      float sd[3];
+      bool scattered = true;
+      if (sc.kind[b] == RT_LAMBERTIAN) {
+        float u[3];
+        unit_vec(unif(r.x), unif(r.y), u[0], u[1], u[2]);
+        for (int a = 0; a < 3; ++a) sd[a] = nn[a] + u[a];
+        const float eps = 1e-8f;
+        if (std::fabs(sd[0]) < eps && std::fabs(sd[1]) < eps && std::fabs(sd[2]) < eps)
+          for (int a = 0; a < 3; ++a) sd[a] = nn[a];
+        th[0] *= sc.ar[b];
+        th[1] *= sc.ag[b];
+        th[2] *= sc.ab[b];
+      } else if (sc.kind[b] == RT_METAL) {
+        const float kk = -2.0f * dot3(d[0], d[1], d[2], nn[0], nn[1], nn[2]);
+        float rf[3], u[3];
+        for (int a = 0; a < 3; ++a) rf[a] = fmaf_(kk, nn[a], d[a]);
+        unit_vec(unif(r.x), unif(r.y), u[0], u[1], u[2]);
+        float fz = sc.param[b];
+        if (!k.metal_unit) fz *= cbrt01(unif(r.z));
+        for (int a = 0; a < 3; ++a) sd[a] = fmaf_(fz, u[a], rf[a]);
+        scattered = dot3(sd[0], sd[1], sd[2], nn[0], nn[1], nn[2]) > 0.0f;
+        th[0] *= sc.ar[b];
+        th[1] *= sc.ag[b];
+        th[2] *= sc.ab[b];
+      } else {
+        const float ratio = front ? 1.0f / sc.param[b] : sc.param[b];
+        const float cos_t = std::fmin(-dot3(d[0], d[1], d[2], nn[0], nn[1], nn[2]), 1.0f);
+        const float sin_t = std::sqrt(fmaf_(-cos_t, cos_t, 1.0f));
+        const bool cannot = ratio * sin_t > 1.0f;
+        float r0 = (1.0f - ratio) / (1.0f + ratio);
+        r0 = r0 * r0;
+        const float x = 1.0f - cos_t;
+        const float x2 = x * x;
+        const float refl = fmaf_(1.0f - r0, x2 * x2 * x, r0);
+        if (cannot || refl > unif(r.x)) {
+          const float kk = -2.0f * dot3(d[0], d[1], d[2], nn[0], nn[1], nn[2]);
+          for (int a = 0; a < 3; ++a) sd[a] = fmaf_(kk, nn[a], d[a]);
+        } else {
+          float q[3];
+          for (int a = 0; a < 3; ++a) q[a] = ratio * fmaf_(cos_t, nn[a], d[a]);
+          const float m = -std::sqrt(std::fabs(1.0f - dot3(q[0], q[1], q[2], q[0], q[1], q[2])));
+          for (int a = 0; a < 3; ++a) sd[a] = fmaf_(m, nn[a], q[a]);
+        }
+      }
+      ++depth;
+      if (!scattered || depth >= k.p->max_depth) break;
+      for (int a = 0; a < 3; ++a) {
+        o[a] = p[a];
+        d[a] = sd[a];
+      }
+      normalize3(d[0], d[1], d[2]);
+    }
+  }
+  return segs;
+}
+
+kscene make_kscene(const rt_scene_view &v) {
+  kscene s;
+  for (uint32_t i = 0; i < v.n; ++i) {
+    const double x = v.cx[i], y = v.cy[i], z = v.cz[i], r = v.radius[i];
+    s.cx.push_back(v.cx[i]);
+    s.cy.push_back(v.cy[i]);
+    s.cz.push_back(v.cz[i]);
+    s.ks.push_back((float)(x * x + y * y + z * z - r * r));
+    s.inv_r.push_back(1.0f / v.radius[i]);
+    s.ar.push_back(v.albedo_rgb[3 * i + 0]);
+    s.ag.push_back(v.albedo_rgb[3 * i + 1]);
+    s.ab.push_back(v.albedo_rgb[3 * i + 2]);
+    s.param.push_back(v.mat_param[i]);
+    s.kind.push_back(v.mat_kind[i]);
+  }
+  return s;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rto_reference_render(int width, double aspect, int spp, int max_depth, int scene,
+                         uint8_t *rgb_out, int *height_out, unsigned long long *segments) {
+  if (width < 2 || !(aspect > 0) || spp < 1 || max_depth < 0) return -1;
+  const int height = (int)(width / aspect);  // main.cc:84
+  if (height < 2) return -1;
+  if (height_out) *height_out = height;
+  if (!rgb_out) return 0;  // size query
+  rng64 r;
+  dworld w;
+  d3 lookfrom{13, 2, 3}, lookat{0, 0, 0};
+  double aperture = 0.1, focus = 10.0;
+  if (scene == 1) {
+    five_scene(w.s);
+    lookfrom = {-2, 2, 1};
+    lookat = {0, 0, -1};
+    aperture = 0.0;
+    focus = 3.4;
+  } else {
+    final_scene(r, 11, w.s);
+  }
+  // camera.h:8-26
+  const double pi = 3.1415926535897932385;
+  double theta = 20.0 * pi / 180.0;
+  double hh = std::tan(theta / 2);
+  double vh = 2.0 * hh, vw = aspect * vh;
+  d3 cw = unit(lookfrom - lookat);
+  d3 cu = unit(cross(d3{0, 1, 0}, cw));
+  d3 cv = cross(cw, cu);
+  d3 origin = lookfrom;
+  d3 horizontal = (focus * vw) * cu;
+  d3 vertical = (focus * vh) * cv;
+  d3 llc = origin - horizontal / 2 - vertical / 2 - focus * cw;
+  double lens_radius = aperture / 2;
+  const double scale = 1.0 / spp;
+  size_t k = 0;
+  for (int j = height - 1; j >= 0; --j) {  // main.cc:111-123
+    for (int i = 0; i < width; ++i) {
+      d3 pc{0, 0, 0};
+      for (int s = 0; s < spp; ++s) {
+        double u = (i + r()) / (width - 1);
+        double v = (j + r()) / (height - 1);
+        d3 rd = lens_radius * in_unit_disk(r);  // camera.h:29-33
+        d3 offset = rd.x * cu + rd.y * cv;
+        d3 ro = origin + offset;
+        d3 rdir = llc + u * horizontal + v * vertical - origin - offset;
+        pc = pc + ray_color(ro, rdir, w, r, max_depth);
+      }
+      rgb_out[k++] = tonemap(pc.x, scale);
+      rgb_out[k++] = tonemap(pc.y, scale);
+      rgb_out[k++] = tonemap(pc.z, scale);
+    }
+  }
+  if (segments) *segments = w.calls;
+  return 0;
+}
+
+int rto_kernel_render(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
+                      float *out, unsigned long long *segments, int threads) {
+  if (!scene || !cam || !p || !out || p->width < 1 || p->height < 1 || p->row_block < 1 ||
+      p->band_stride < 1 || p->local_rows < 0)
+    return -1;
+  const kscene sc = make_kscene(*scene);
+  kctx k{&sc, cam, p, (uint32_t)p->seed ^ ((uint32_t)(p->seed >> 32) * 0x9E3779B9u),
+         (p->flags & RT_FLAG_OPEN_INTERVAL) != 0, (p->flags & RT_FLAG_METAL_UNIT_VECTOR) != 0};
+  if (threads < 1) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+  std::atomic<int> next_row{0};
+  std::atomic<unsigned long long> total{0};
+  auto worker = [&]() {
+    unsigned long long segs = 0;
+    for (int lr; (lr = next_row.fetch_add(1)) < p->local_rows;) {
+      const int band = lr / p->row_block;
+      const int grow = (band * p->band_stride + p->band_offset) * p->row_block + lr % p->row_block;
+      for (int col = 0; col < p->width; ++col) {
+        float *o = out + 3 * ((size_t)lr * p->width + col);
+        if (grow >= p->height) {
+          o[0] = o[1] = o[2] = 0.0f;
+          continue;
+        }
+        segs += kernel_pixel(k, col, grow, o);
+      }
+    }
+    total += segs;
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; ++t) pool.emplace_back(worker);
+  worker();
+  for (auto &t : pool) t.join();
+  if (segments) *segments = total.load();
+  return 0;
+}
+
+int rto_reference_scene(int half_extent, double *rows, size_t capacity, size_t *n_out,
+                        double *rng_next) {
+  rng64 r;
+  std::vector<dsphere> s;
+  final_scene(r, half_extent, s);
+  if (n_out) *n_out = s.size();
+  if (rng_next) *rng_next = r();
+  if (!rows) return 0;
+  if (capacity < s.size()) return -1;
+  for (size_t i = 0; i < s.size(); ++i) {
+    double *q = rows + 9 * i;
+    q[0] = s[i].kind;
+    q[1] = s[i].c.x;
+    q[2] = s[i].c.y;
+    q[3] = s[i].c.z;
+    q[4] = s[i].r;
+    q[5] = s[i].albedo.x;
+    q[6] = s[i].albedo.y;
+    q[7] = s[i].albedo.z;
+    q[8] = s[i].param;
+  }
+  return 0;
+}
+
+}  // extern "C"

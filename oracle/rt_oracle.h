@@ -1,0 +1,26 @@
+/* oracle/rt_oracle.h -- TEST INFRASTRUCTURE ONLY (see rt_oracle.cc).
+ * C ABI of the CPU restatement; loaded by tests/ via ctypes. */
+#ifndef RTOW_ORACLE_H
+#define RTOW_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+#include "rt.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* fp64 restatement of src/cpu: height = (int)(width/aspect); writes
+ * width*height*3 tonemapped bytes, TOP row first (src/cpu/main.cc:109-123).
+ * scene 0 = final random scene (main.cc:32-76), 1 = five-sphere book scene.
+ * rgb_out == NULL: size query (fills *height_out). */
+int rto_reference_render(int width, double aspect, int spp, int max_depth, int scene,
+                         uint8_t *rgb_out, int *height_out, unsigned long long *segments);
+/* fp32 restatement of the kernel algorithm; same arguments as rt_render. */
+int rto_kernel_render(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
+                      float *out, unsigned long long *segments, int threads);
+/* fp64 final scene rows: kind, cx, cy, cz, r, albedo rgb, param (9 doubles). */
+int rto_reference_scene(int half_extent, double *rows, size_t capacity, size_t *n_out,
+                        double *rng_next);
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,237 @@
+// cli.cpp -- drop-in process surface for cpu_ray_tracer / gpu_ray_tracer.
+//
+// Same conventions as the reference executables: P3 PPM on stdout, progress
+// and timing on stderr (src/cpu/main.cc:103-132, src/gpu/main.cu:121-139),
+// exit code 99 on a device error (src/gpu/cuda_utility.h:8-18).  The
+// personality is chosen by argv[0]:
+//   cpu_ray_tracer : 1200x800 (3:2), 500 spp, depth 50, src/cpu camera and
+//                    semantics (src/cpu/main.cc:82-99)
+//   gpu_ray_tracer : 1920x1080 (16:9), 500 spp, depth 50, src/gpu camera
+//                    (defocus 0.6 deg) and semantics, seed = time(nullptr)
+//                    (src/gpu/main.cu:88, src/gpu/camera.h:58-71)
+//   rtow           : cpu_ray_tracer defaults
+// Everything renders on the GPU through librtow.so; flags override defaults:
+//   --width N --height N --spp N --depth N --seed N --spheres K (grid half
+//   extent; 11 = reference, 50 = 10k spheres) --scene final|five
+//   --camera cpu|gpu --semantics cpu|gpu --gpus N --device N --out FILE --p6
+//   --quiet
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "rt.h"
+
+namespace {
+
+struct options {
+  int width = 1200, height = 800, spp = 500, depth = 50;
+  unsigned long long seed = 0;
+  bool seed_set = false;
+  int half_extent = 11;
+  std::string scene = "final";
+  int camera = RT_CAMERA_CPU;
+  unsigned flags = 0;
+  int gpus = 1, device = 0;
+  std::string out;
+  bool p6 = false, quiet = false;
+};
+
+[[noreturn]] void die(const char *what, int st) {
+  std::fprintf(stderr, "rtow error = %d (%s) at '%s'\n", st, rt_strerror(st), what);
+  std::exit(99);  // src/gpu/cuda_utility.h:16
+}
+
+void check(int st, const char *what) {
+  if (st != RT_OK) die(what, st);
+}
+
+[[noreturn]] void usage(const char *argv0) {
+  std::fprintf(stderr,
+               "usage: %s [--width N] [--height N] [--spp N] [--depth N] [--seed N]\n"
+               "          [--spheres HALF_EXTENT] [--scene final|five] [--camera cpu|gpu]\n"
+               "          [--semantics cpu|gpu] [--gpus N] [--device N] [--out FILE] [--p6] [--quiet]\n",
+               argv0);
+  std::exit(2);
+}
+
+struct gpu_job {
+  int device;
+  rt_params params;
+  std::vector<float> host;
+  rt_stats stats{};
+  int status = RT_OK;
+};
+
+}  // namespace
+
+int main(int argc, char **argv) {
+  options o;
+  std::string name = argv[0];
+  if (auto s = name.rfind('/'); s != std::string::npos) name = name.substr(s + 1);
+  const bool gpu_mode = name == "gpu_ray_tracer";
+  if (gpu_mode) {
+    o.width = 1920;
+    o.height = 1080;  // static_cast<int>(1920 / (16/9)), src/gpu/camera.h:60-62
+    o.camera = RT_CAMERA_GPU;
+    o.flags = RT_FLAG_GPU_SEMANTICS;
+  }
+  bool height_set = false;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto next = [&]() -> const char * {
+      if (i + 1 >= argc) usage(argv[0]);
+      return argv[++i];
+    };
+    if (a == "--width") o.width = std::atoi(next());
+    else if (a == "--height") { o.height = std::atoi(next()); height_set = true; }
+    else if (a == "--spp") o.spp = std::atoi(next());
+    else if (a == "--depth") o.depth = std::atoi(next());
+    else if (a == "--seed") { o.seed = std::strtoull(next(), nullptr, 10); o.seed_set = true; }
+    else if (a == "--spheres") o.half_extent = std::atoi(next());
+    else if (a == "--scene") o.scene = next();
+    else if (a == "--camera") o.camera = std::string(next()) == "gpu" ? RT_CAMERA_GPU : RT_CAMERA_CPU;
+    else if (a == "--semantics") o.flags = std::string(next()) == "gpu" ? RT_FLAG_GPU_SEMANTICS : 0u;
+    else if (a == "--gpus") o.gpus = std::atoi(next());
+    else if (a == "--device") o.device = std::atoi(next());
+    else if (a == "--out") o.out = next();
+    else if (a == "--p6") o.p6 = true;
+    else if (a == "--quiet") o.quiet = true;
+    else usage(argv[0]);
+  }
+  if (!height_set && (o.width != (gpu_mode ? 1920 : 1200))) {
+    // keep the reference aspect ratio when only the width is given
+    o.height = gpu_mode ? (int)(o.width / (16.0f / 9.0f)) : (int)(o.width / (3.0 / 2.0));
+  }
+  if (gpu_mode && !o.seed_set) o.seed = (unsigned long long)std::time(nullptr);  // main.cu:88
+  if (o.width < 2 || o.height < 2 || o.spp < 0 || o.depth < 0 || o.gpus < 1) usage(argv[0]);
+
+  // ---- scene (random_scene / new_world) ----
+  const uint32_t cap = (uint32_t)(4 * o.half_extent * o.half_extent + 16);
+  std::vector<float> cx(cap), cy(cap), cz(cap), rad(cap), alb(3 * cap), par(cap);
+  std::vector<uint32_t> kind(cap);
+  rt_scene_buf buf{cap, 0, cx.data(), cy.data(), cz.data(), rad.data(), kind.data(), alb.data(), par.data()};
+  if (o.scene == "five") check(rt_scene_five(&buf), "rt_scene_five");
+  else check(rt_scene_final(o.half_extent, &buf, nullptr), "rt_scene_final");
+  rt_scene_view view{buf.n, cx.data(), cy.data(), cz.data(), rad.data(), kind.data(), alb.data(), par.data()};
+
+  // ---- camera ----
+  rt_camera cam;
+  const bool five = o.scene == "five";
+  const double from_f[3] = {13, 2, 3}, at_f[3] = {0, 0, 0};
+  const double from_5[3] = {-2, 2, 1}, at_5[3] = {0, 0, -1};
+  const double vup[3] = {0, 1, 0};
+  const double *from = five ? from_5 : from_f, *at = five ? at_5 : at_f;
+  if (o.camera == RT_CAMERA_GPU)
+    check(rt_camera_gpu(from, at, vup, 20.0, o.width, o.height, five ? 10.0 : 0.6, five ? 3.4 : 10.0, &cam),
+          "rt_camera_gpu");
+  else
+    check(rt_camera_cpu(from, at, vup, 20.0, (double)o.width / o.height, five ? 0.0 : 0.1,
+                        five ? 3.4 : 10.0, &cam),
+          "rt_camera_cpu");
+
+  int ndev = 0;
+  check(rt_device_count(&ndev), "rt_device_count");
+  if (ndev < 1) die("no HIP device", RT_ERR_NO_DEVICE);
+  if (o.gpus > ndev) o.gpus = ndev;
+
+  if (!o.quiet) {
+    std::fprintf(stderr, "Image Size = %d x %d\n", o.width, o.height);
+    std::fprintf(stderr, "Samples Per Pixel = %d\n", o.spp);
+    std::fprintf(stderr, "Number of GPUs = %d (wave64 tiles of 8 x 8 pixels)\n", o.gpus);
+    std::fprintf(stderr, "Spheres = %u\n", buf.n);
+    if (gpu_mode || o.seed_set) std::fprintf(stderr, "Random Seed = %llu\n", o.seed);
+  }
+
+  // ---- render: one host thread + context per GPU, interleaved row bands ----
+  const int row_block = 8;
+  std::vector<gpu_job> jobs(o.gpus);
+  for (int g = 0; g < o.gpus; ++g) {
+    rt_params p{};
+    p.width = o.width;
+    p.height = o.height;
+    p.spp = o.spp;
+    p.max_depth = o.depth;
+    p.seed = o.seed;
+    p.flags = o.flags;
+    if (o.gpus == 1) {
+      p.row_block = o.height;
+      p.band_stride = 1;
+      p.band_offset = 0;
+      p.local_rows = o.height;
+    } else {
+      const int band_rows = row_block * o.gpus;
+      p.row_block = row_block;
+      p.band_stride = o.gpus;
+      p.band_offset = g;
+      p.local_rows = (o.height + band_rows - 1) / band_rows * row_block;
+    }
+    jobs[g].device = o.gpus == 1 ? o.device : g;
+    jobs[g].params = p;
+    jobs[g].host.resize(3 * (size_t)p.width * p.local_rows);
+  }
+  std::vector<rt_context *> ctxs(o.gpus, nullptr);
+  for (int g = 0; g < o.gpus; ++g) {
+    check(rt_context_create(jobs[g].device, &ctxs[g]), "rt_context_create");
+    check(rt_scene_upload(ctxs[g], &view), "rt_scene_upload");
+  }
+  auto start = std::chrono::high_resolution_clock::now();
+  std::vector<std::thread> threads;
+  for (int g = 0; g < o.gpus; ++g)
+    threads.emplace_back([&, g]() {
+      jobs[g].status = rt_render(ctxs[g], &cam, &jobs[g].params, jobs[g].host.data(), &jobs[g].stats);
+    });
+  for (auto &t : threads) t.join();
+  auto end = std::chrono::high_resolution_clock::now();
+  for (int g = 0; g < o.gpus; ++g) check(jobs[g].status, "rt_render");
+
+  // main.cu:134-139 timing lines
+  float ms = std::chrono::duration<float, std::milli>(end - start).count();
+  int time_cost_in_ms = (int)(ms + 0.999f);
+  int time_cost_in_sec = (time_cost_in_ms + 999) / 1000;
+  unsigned long long segs = 0, samples = 0;
+  for (auto &j : jobs) {
+    segs += j.stats.segments;
+    samples += j.stats.samples;
+  }
+  if (!o.quiet) {
+    std::fprintf(stderr, "Time Cost (ms) = %d ms\n", time_cost_in_ms);
+    std::fprintf(stderr, "Time Cost (sec) = %d sec\n", time_cost_in_sec);
+    std::fprintf(stderr, "Throughput = %.1f Mray/s, %.1f Msample/s (%llu segments)\n",
+                 segs / (ms * 1e3), samples / (ms * 1e3), segs);
+  }
+
+  // ---- assemble + tonemap + PPM (output_image, src/gpu/camera.h:197-210) ----
+  std::vector<float> frame(3 * (size_t)o.width * o.height, 0.0f);
+  for (int g = 0; g < o.gpus; ++g) {
+    const rt_params &p = jobs[g].params;
+    for (int r = 0; r < p.local_rows; ++r) {
+      const int band = r / p.row_block;
+      const int grow = (band * p.band_stride + p.band_offset) * p.row_block + r % p.row_block;
+      if (grow >= o.height) continue;
+      std::memcpy(&frame[3 * (size_t)grow * o.width], &jobs[g].host[3 * (size_t)r * o.width],
+                  3 * sizeof(float) * o.width);
+    }
+  }
+  std::vector<uint8_t> rgb(frame.size());
+  check(rt_tonemap_u8(frame.data(), (size_t)o.width * o.height, o.spp > 0 ? o.spp : 1, rgb.data()),
+        "rt_tonemap_u8");
+  int fd = 1;
+  if (!o.out.empty()) {
+    fd = ::open(o.out.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0) die(o.out.c_str(), RT_ERR_IO);
+  }
+  check(rt_write_ppm(fd, rgb.data(), o.width, o.height, o.p6 ? 1 : 0), "rt_write_ppm");
+  if (fd != 1) ::close(fd);
+  for (auto *c : ctxs) rt_context_destroy(c);
+  if (!o.quiet) std::fprintf(stderr, "\nDone.\n");
+  return 0;
+}

@@ -1,0 +1,678 @@
+// rt_render.hip -- the MI355X (gfx950) render kernel and the device half of
+// the C ABI in include/rt.h.
+//
+// Replaces render<<<>>> (src/gpu/camera.h:169-195) and, inside it, get_ray
+// (camera.h:153-167 / src/cpu/camera.h:28-34), ray_color (src/cpu/main.cc:12-30,
+// iterative as in src/gpu/camera.h:112-138), hittable_list::hit / sphere::hit
+// (src/cpu/hittable_list.h:28-43, src/cpu/sphere.h:24-51) and the three
+// material::scatter functions (src/cpu/material.h:15-88).
+//
+// Design (DESIGN.md "Kernel"):
+//  * one lane per pixel, one wave64 per 8x8 pixel tile, 4 waves per block;
+//  * the lane loops over ITS pixel's spp samples and regenerates a camera ray
+//    as soon as a path ends ("path regeneration"), so every bounce iteration
+//    of the wave does useful work on every lane until that lane's pixel is
+//    finished; the wave exits on __ballot(alive) == 0;
+//  * the closest-hit scan walks the sphere array with a wave-uniform index:
+//    sphere data are scalar (SMEM) loads into SGPRs that feed the VALU
+//    directly -- 7 FMAs + 1 compare per ray-sphere test, no LDS traffic, no
+//    per-sphere divergence; the square root and the interval test run only
+//    in the (rare) branch where some lane's discriminant is non-negative;
+//  * counter-based RNG (pcg4d keyed by pixel, sample, bounce slot, seed):
+//    no per-pixel state, results independent of launch geometry and of the
+//    number of GPUs;
+//  * fp32 with explicit fmaf and -ffp-contract=off: the kernel is bit-exact
+//    with the CPU restatement in oracle/rt_oracle.cc (kernel mode).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <new>
+
+#include "rt.h"
+
+extern "C" void rt_internal_set_hip_error(int e);
+
+namespace rtk {
+
+constexpr int kTile = 8;           // 8x8 pixels per wave
+constexpr int kWavesPerBlock = 4;  // 256 threads
+constexpr int kBlock = 64 * kWavesPerBlock;
+constexpr int kSpherePad = 8;      // scan unroll granularity
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// scan record for two consecutive spheres i, i+1 (32 B): every field is a
+// pair so that one s_load_dwordx8 yields ready-made SGPR pairs
+struct __attribute__((aligned(32))) pair_geom {
+  f2 cx, cy, cz, ks;  // ks = |C|^2 - r^2
+};
+
+// per-sphere shading record, fetched once per segment for the closest sphere
+struct __attribute__((aligned(16))) shade_rec {
+  float cx, cy, cz, inv_r;
+  float ar, ag, ab, param;
+  uint32_t kind, pad0, pad1, pad2;
+};
+
+struct kparams {
+  rt_camera cam;
+  int width, height, spp, max_depth;
+  int row_block, band_stride, band_offset, local_rows;
+  int tiles_x, n_pad;
+  uint32_t seed32, flags;
+  float wm1, hm1;  // (float)(W-1), (float)(H-1)  (cpu camera model)
+};
+
+// ---------------------------------------------------------------- RNG ----
+// pcg4d (Jarzynski & Olano, "Hash Functions for GPU Rendering", JCGT 2020):
+// a 4-D -> 4-D counter hash; one call gives the 4 uniforms a bounce needs.
+__device__ __forceinline__ uint4 pcg4d(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  uint32_t x = a * 1664525u + 1013904223u;
+  uint32_t y = b * 1664525u + 1013904223u;
+  uint32_t z = c * 1664525u + 1013904223u;
+  uint32_t w = d * 1664525u + 1013904223u;
+  x += y * w; y += z * x; z += x * y; w += y * z;
+  x ^= x >> 16; y ^= y >> 16; z ^= z >> 16; w ^= w >> 16;
+  x += y * w; y += z * x; z += x * y; w += y * z;
+  return make_uint4(x, y, z, w);
+}
+
+__device__ __forceinline__ float unif(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
+
+// sin/cos of 2*pi*u, u in [0,1): quadrant from 4u (exact), Taylor on [0,pi/2).
+__device__ __forceinline__ void sincos_turn(float u, float &s, float &c) {
+  float q4 = u * 4.0f;
+  float qf = floorf(q4);
+  int q = (int)qf;
+  float x = (q4 - qf) * 1.57079632679489662f;
+  float x2 = x * x;
+  float sp = fmaf(x2, -2.50521084e-08f, 2.75573192e-06f);
+  sp = fmaf(x2, sp, -1.98412698e-04f);
+  sp = fmaf(x2, sp, 8.33333333e-03f);
+  sp = fmaf(x2, sp, -1.66666667e-01f);
+  sp = fmaf(x2, sp, 1.0f);
+  float sn = x * sp;
+  float cp = fmaf(x2, 2.08767570e-09f, -2.75573192e-07f);
+  cp = fmaf(x2, cp, 2.48015873e-05f);
+  cp = fmaf(x2, cp, -1.38888889e-03f);
+  cp = fmaf(x2, cp, 4.16666667e-02f);
+  cp = fmaf(x2, cp, -0.5f);
+  float cs = fmaf(x2, cp, 1.0f);
+  float s0 = (q & 1) ? cs : sn;
+  float c0 = (q & 1) ? sn : cs;
+  s = (q & 2) ? -s0 : s0;
+  c = ((q + 1) & 2) ? -c0 : c0;
+}
+
+// cube root of u in [0,1): bit-hack seed + 3 Newton steps (same ops on host).
+__device__ __forceinline__ float cbrt01(float u) {
+  uint32_t i = __float_as_uint(u) / 3u + 709921077u;
+  float y = __uint_as_float(i);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    float y2 = y * y;
+    y = fmaf(y, 0.666666687f, (u / y2) * 0.333333343f);
+  }
+  return u == 0.0f ? 0.0f : y;
+}
+
+// uniform direction on the unit sphere (replaces the rejection loop of
+// random_unit_vector, src/cpu/vec3.h:105-114; equal in distribution)
+__device__ __forceinline__ void unit_vec(float u1, float u2, float &x, float &y, float &z) {
+  z = fmaf(-2.0f, u1, 1.0f);
+  float r = sqrtf(fmaxf(fmaf(-z, z, 1.0f), 0.0f));
+  float s, c;
+  sincos_turn(u2, s, c);
+  x = r * c;
+  y = r * s;
+}
+
+__device__ __forceinline__ void normalize3(float &x, float &y, float &z) {
+  float l2 = fmaf(z, z, fmaf(y, y, x * x));
+  float inv = 1.0f / sqrtf(l2);
+  x *= inv;
+  y *= inv;
+  z *= inv;
+}
+
+__device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {
+  return fmaf(az, bz, fmaf(ay, by, ax * bx));
+}
+
+// camera ray for (pixel, sample): get_ray, src/cpu/camera.h:28-34 (model CPU)
+// or src/gpu/camera.h:153-167 (model GPU)
+__device__ __forceinline__ void camera_ray(const kparams &p, uint32_t pix, int col, int grow,
+                                           uint32_t sample, float &ox, float &oy, float &oz,
+                                           float &dx, float &dy, float &dz) {
+  uint4 r = pcg4d(pix, sample, 0u, p.seed32);
+  float u1 = unif(r.x), u2 = unif(r.y);
+  float fs, ft;
+  if (p.cam.model == RT_CAMERA_CPU) {
+    int j = p.height - 1 - grow;
+    fs = ((float)col + u1) / p.wm1;
+    ft = ((float)j + u2) / p.hm1;
+  } else {
+    fs = (float)col + (u1 - 0.5f);
+    ft = (float)grow + (u2 - 0.5f);
+  }
+  float tx = fmaf(ft, p.cam.vert[0], fmaf(fs, p.cam.horiz[0], p.cam.corner[0]));
+  float ty = fmaf(ft, p.cam.vert[1], fmaf(fs, p.cam.horiz[1], p.cam.corner[1]));
+  float tz = fmaf(ft, p.cam.vert[2], fmaf(fs, p.cam.horiz[2], p.cam.corner[2]));
+  ox = p.cam.eye[0];
+  oy = p.cam.eye[1];
+  oz = p.cam.eye[2];
+  if (p.cam.has_lens) {
+    float rr = sqrtf(unif(r.z));
+    float s, c;
+    sincos_turn(unif(r.w), s, c);
+    float ddx = rr * c, ddy = rr * s;
+    ox = fmaf(ddy, p.cam.lens_v[0], fmaf(ddx, p.cam.lens_u[0], ox));
+    oy = fmaf(ddy, p.cam.lens_v[1], fmaf(ddx, p.cam.lens_u[1], oy));
+    oz = fmaf(ddy, p.cam.lens_v[2], fmaf(ddx, p.cam.lens_u[2], oz));
+  }
+  dx = tx - ox;
+  dy = ty - oy;
+  dz = tz - oz;
+  normalize3(dx, dy, dz);
+}
+
+template <bool OPEN>
+__device__ __forceinline__ bool in_range(float t, float tmin, float tmax) {
+  if (OPEN) return (t > tmin) & (t < tmax);   // interval::surrounds
+  return (t >= tmin) & (t <= tmax);           // src/cpu/sphere.h:38-42
+}
+
+// closest-hit candidate update (sphere.h:34-44 with a = |d|^2 = 1)
+template <bool OPEN>
+__device__ __forceinline__ void candidate(bool c, float h, float disc, int idx, float &tmax,
+                                          int &best) {
+  if (c) {
+    float sq = sqrtf(disc);
+    float t0 = h - sq, t1 = h + sq;
+    bool ok0 = in_range<OPEN>(t0, 0.001f, tmax);
+    bool ok1 = in_range<OPEN>(t1, 0.001f, tmax);
+    if (ok0 | ok1) {
+      tmax = ok0 ? t0 : t1;
+      best = idx;
+    }
+  }
+}
+
+template <bool OPEN, bool METAL_UNIT>
+__global__ __launch_bounds__(kBlock) void render_kernel(const kparams p,
+                                                        const pair_geom *__restrict__ geom,
+                                                        const shade_rec *__restrict__ shade,
+                                                        float *__restrict__ out,
+                                                        unsigned long long *__restrict__ counters) {
+  const int lane = threadIdx.x & 63;
+  const int tile = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int tx = tile % p.tiles_x, ty = tile / p.tiles_x;
+  const int col = tx * kTile + (lane & (kTile - 1));
+  const int lrow = ty * kTile + (lane >> 3);
+  const int band = lrow / p.row_block;
+  const int grow = (band * p.band_stride + p.band_offset) * p.row_block + (lrow - band * p.row_block);
+  const bool in_tile = col < p.width && lrow < p.local_rows;
+  const bool valid = in_tile && grow < p.height;
+  const uint32_t pix = (uint32_t)grow * (uint32_t)p.width + (uint32_t)col;
+
+  float accr = 0.f, accg = 0.f, accb = 0.f;
+  float ox = 0.f, oy = 0.f, oz = 0.f, dx = 0.f, dy = 1.f, dz = 0.f;
+  float thr = 1.f, thg = 1.f, thb = 1.f;
+  int depth = 0;
+  uint32_t sample = 0;
+  uint32_t segs = 0, steps = 0;
+  bool alive = valid && p.spp > 0 && p.max_depth > 0;  // depth 0: black, no hit test
+  if (alive) {
+    camera_ray(p, pix, col, grow, 0u, ox, oy, oz, dx, dy, dz);
+    sample = 1;
+  }
+
+  const int n_pairs = p.n_pad / 2;
+  while (__ballot(alive)) {
+    ++steps;
+    if (alive) {
+      ++segs;
+      // ---- closest hit over all spheres (hittable_list::hit) ----
+      const float nk1 = -dot3(ox, oy, oz, dx, dy, dz);
+      const float o2 = dot3(ox, oy, oz, ox, oy, oz);
+      const float ox2 = -2.0f * ox, oy2 = -2.0f * oy, oz2 = -2.0f * oz;
+      float tmax = __builtin_huge_valf();
+      int best = -1;
+      const f2 vdx = {dx, dx}, vdy = {dy, dy}, vdz = {dz, dz};
+      const f2 vnk1 = {nk1, nk1}, vo2 = {o2, o2};
+      const f2 vox2 = {ox2, ox2}, voy2 = {oy2, oy2}, voz2 = {oz2, oz2};
+      // 8 spheres (4 pairs) per iteration; the pair layout puts (x_i, x_i+1)
+      // in one SGPR pair, so each v_pk_fma_f32 tests two spheres.
+      for (int k = 0; k < n_pairs; k += 4) {
+        const pair_geom q0 = geom[k + 0];
+        const pair_geom q1 = geom[k + 1];
+        const pair_geom q2 = geom[k + 2];
+        const pair_geom q3 = geom[k + 3];
+        const f2 h0 = fma2(q0.cz, vdz, fma2(q0.cy, vdy, fma2(q0.cx, vdx, vnk1)));
+        const f2 h1 = fma2(q1.cz, vdz, fma2(q1.cy, vdy, fma2(q1.cx, vdx, vnk1)));
+        const f2 h2 = fma2(q2.cz, vdz, fma2(q2.cy, vdy, fma2(q2.cx, vdx, vnk1)));
+        const f2 h3 = fma2(q3.cz, vdz, fma2(q3.cy, vdy, fma2(q3.cx, vdx, vnk1)));
+        const f2 g0 = fma2(q0.cz, voz2, fma2(q0.cy, voy2, fma2(q0.cx, vox2, vo2)));
+        const f2 g1 = fma2(q1.cz, voz2, fma2(q1.cy, voy2, fma2(q1.cx, vox2, vo2)));
+        const f2 g2 = fma2(q2.cz, voz2, fma2(q2.cy, voy2, fma2(q2.cx, vox2, vo2)));
+        const f2 g3 = fma2(q3.cz, voz2, fma2(q3.cy, voy2, fma2(q3.cx, vox2, vo2)));
+        const f2 e0 = fma2(h0, h0, -g0);
+        const f2 e1 = fma2(h1, h1, -g1);
+        const f2 e2 = fma2(h2, h2, -g2);
+        const f2 e3 = fma2(h3, h3, -g3);
+        // discriminant >= 0  <=>  e >= ks  (exact for finite floats)
+        const bool c0 = e0.x >= q0.ks.x, c1 = e0.y >= q0.ks.y;
+        const bool c2 = e1.x >= q1.ks.x, c3 = e1.y >= q1.ks.y;
+        const bool c4 = e2.x >= q2.ks.x, c5 = e2.y >= q2.ks.y;
+        const bool c6 = e3.x >= q3.ks.x, c7 = e3.y >= q3.ks.y;
+        const uint64_t any = __builtin_amdgcn_ballot_w64(c0) | __builtin_amdgcn_ballot_w64(c1) |
+                             __builtin_amdgcn_ballot_w64(c2) | __builtin_amdgcn_ballot_w64(c3) |
+                             __builtin_amdgcn_ballot_w64(c4) | __builtin_amdgcn_ballot_w64(c5) |
+                             __builtin_amdgcn_ballot_w64(c6) | __builtin_amdgcn_ballot_w64(c7);
+        if (any) {  // wave-uniform: the rare path where some line meets a sphere
+          const int i = 2 * k;
+          candidate<OPEN>(c0, h0.x, e0.x - q0.ks.x, i + 0, tmax, best);
+          candidate<OPEN>(c1, h0.y, e0.y - q0.ks.y, i + 1, tmax, best);
+          candidate<OPEN>(c2, h1.x, e1.x - q1.ks.x, i + 2, tmax, best);
+          candidate<OPEN>(c3, h1.y, e1.y - q1.ks.y, i + 3, tmax, best);
+          candidate<OPEN>(c4, h2.x, e2.x - q2.ks.x, i + 4, tmax, best);
+          candidate<OPEN>(c5, h2.y, e2.y - q2.ks.y, i + 5, tmax, best);
+          candidate<OPEN>(c6, h3.x, e3.x - q3.ks.x, i + 6, tmax, best);
+          candidate<OPEN>(c7, h3.y, e3.y - q3.ks.y, i + 7, tmax, best);
+        }
+      }
+
+      bool path_done = false;
+      if (best < 0) {
+        // miss: sky gradient, src/cpu/main.cc:27-29
+        const float a = 0.5f * (dy + 1.0f);
+        const float s0 = 1.0f - a;
+        accr = fmaf(thr, fmaf(a, 0.5f, s0), accr);
+        accg = fmaf(thg, fmaf(a, 0.7f, s0), accg);
+        accb = fmaf(thb, s0 + a, accb);
+        path_done = true;
+      } else {
+        const shade_rec sr = shade[best];
+        const float px = fmaf(tmax, dx, ox), py = fmaf(tmax, dy, oy), pz = fmaf(tmax, dz, oz);
+        float nx = (px - sr.cx) * sr.inv_r, ny = (py - sr.cy) * sr.inv_r, nz = (pz - sr.cz) * sr.inv_r;
+        const bool front = dot3(dx, dy, dz, nx, ny, nz) < 0.0f;  // hittable.h:16-19
+        if (!front) {
+          nx = -nx;
+          ny = -ny;
+          nz = -nz;
+        }
+        const uint4 r = pcg4d(pix, sample - 1u, (uint32_t)(depth + 1), p.seed32);
+        float sx, sy, sz;
+        bool scattered = true;
+        if (sr.kind == RT_LAMBERTIAN) {
+          // material.h:19-30
+          float ux, uy, uz;
+          unit_vec(unif(r.x), unif(r.y), ux, uy, uz);
+          sx = nx + ux;
+          sy = ny + uy;
+          sz = nz + uz;
+          const float e = 1e-8f;
+          if (fabsf(sx) < e && fabsf(sy) < e && fabsf(sz) < e) {
+            sx = nx;
+            sy = ny;
+            sz = nz;
+          }
+          thr *= sr.ar;
+          thg *= sr.ag;
+          thb *= sr.ab;
+        } else if (sr.kind == RT_METAL) {
+          // material.h:40-46
+          const float k = -2.0f * dot3(dx, dy, dz, nx, ny, nz);
+          const float rx = fmaf(k, nx, dx), ry = fmaf(k, ny, dy), rz = fmaf(k, nz, dz);
+          float ux, uy, uz;
+          unit_vec(unif(r.x), unif(r.y), ux, uy, uz);
+          float fz = sr.param;
+          if (!METAL_UNIT) fz *= cbrt01(unif(r.z));  // random_in_unit_sphere
+          sx = fmaf(fz, ux, rx);
+          sy = fmaf(fz, uy, ry);
+          sz = fmaf(fz, uz, rz);
+          scattered = dot3(sx, sy, sz, nx, ny, nz) > 0.0f;
+          thr *= sr.ar;
+          thg *= sr.ag;
+          thb *= sr.ab;
+        } else {
+          // dielectric, material.h:57-87
+          const float ratio = front ? 1.0f / sr.param : sr.param;
+          const float cos_t = fminf(-dot3(dx, dy, dz, nx, ny, nz), 1.0f);
+          const float sin_t = sqrtf(fmaf(-cos_t, cos_t, 1.0f));
+          const bool cannot = ratio * sin_t > 1.0f;
+          float r0 = (1.0f - ratio) / (1.0f + ratio);
+          r0 = r0 * r0;
+          const float x = 1.0f - cos_t;
+          const float x2 = x * x;
+          const float refl = fmaf(1.0f - r0, x2 * x2 * x, r0);
+          if (cannot || refl > unif(r.x)) {
+            const float k = -2.0f * dot3(dx, dy, dz, nx, ny, nz);
+            sx = fmaf(k, nx, dx);
+            sy = fmaf(k, ny, dy);
+            sz = fmaf(k, nz, dz);
+          } else {
+            const float qx = ratio * fmaf(cos_t, nx, dx);
+            const float qy = ratio * fmaf(cos_t, ny, dy);
+            const float qz = ratio * fmaf(cos_t, nz, dz);
+            const float m = -sqrtf(fabsf(1.0f - dot3(qx, qy, qz, qx, qy, qz)));
+            sx = fmaf(m, nx, qx);
+            sy = fmaf(m, ny, qy);
+            sz = fmaf(m, nz, qz);
+          }
+        }
+        ++depth;
+        if (!scattered || depth >= p.max_depth) {
+          path_done = true;  // absorbed, or bounce limit (main.cc:16-17): black
+        } else {
+          ox = px;
+          oy = py;
+          oz = pz;
+          dx = sx;
+          dy = sy;
+          dz = sz;
+          normalize3(dx, dy, dz);
+        }
+      }
+      if (path_done) {
+        if (sample < (uint32_t)p.spp) {
+          camera_ray(p, pix, col, grow, sample, ox, oy, oz, dx, dy, dz);
+          ++sample;
+          depth = 0;
+          thr = thg = thb = 1.0f;
+        } else {
+          alive = false;
+        }
+      }
+    }
+  }
+
+  if (in_tile) {
+    float *o = out + 3 * ((size_t)lrow * p.width + col);
+    o[0] = accr;
+    o[1] = accg;
+    o[2] = accb;
+  }
+  // one atomic per wave for the counters
+  uint32_t s = segs;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if (lane == 0) {
+    atomicAdd(&counters[0], (unsigned long long)s);
+    atomicAdd(&counters[1], (unsigned long long)steps);
+  }
+}
+
+}  // namespace rtk
+
+// ------------------------------------------------------------ context ----
+struct rt_context {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  rtk::pair_geom *d_geom = nullptr;
+  rtk::shade_rec *d_shade = nullptr;
+  uint32_t n_spheres = 0, n_pad = 0;
+  unsigned long long *d_counters = nullptr;
+  float *d_frame = nullptr;
+  size_t frame_floats = 0;
+  uint64_t last_samples = 0;
+};
+
+namespace {
+
+int hip_fail(hipError_t e) {
+  rt_internal_set_hip_error((int)e);
+  return RT_ERR_HIP;
+}
+
+#define RT_HIP(call)                         \
+  do {                                       \
+    hipError_t _e = (call);                  \
+    if (_e != hipSuccess) return hip_fail(_e); \
+  } while (0)
+
+bool params_ok(const rt_params *p) {
+  return p && p->width >= 1 && p->height >= 1 && p->spp >= 0 && p->max_depth >= 0 &&
+         p->row_block >= 1 && p->band_stride >= 1 && p->band_offset >= 0 &&
+         p->band_offset < p->band_stride && p->local_rows >= 0 &&
+         (uint64_t)p->width * (uint64_t)p->height < (1ull << 32);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_device_count(int *count) {
+  if (!count) return RT_ERR_INVALID;
+  hipError_t e = hipGetDeviceCount(count);
+  if (e == hipErrorNoDevice) {
+    *count = 0;
+    return RT_OK;
+  }
+  if (e != hipSuccess) return hip_fail(e);
+  return RT_OK;
+}
+
+int rt_context_create(int device_ordinal, rt_context **out) {
+  if (!out) return RT_ERR_INVALID;
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || device_ordinal < 0 || device_ordinal >= n) {
+    if (e != hipSuccess) rt_internal_set_hip_error((int)e);
+    return RT_ERR_NO_DEVICE;
+  }
+  rt_context *c = new (std::nothrow) rt_context();
+  if (!c) return RT_ERR_NOMEM;
+  c->device = device_ordinal;
+  int st = RT_OK;
+  do {
+    if ((e = hipSetDevice(device_ordinal)) != hipSuccess) break;
+    if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) break;
+    if ((e = hipEventCreate(&c->ev0)) != hipSuccess) break;
+    if ((e = hipEventCreate(&c->ev1)) != hipSuccess) break;
+    if ((e = hipMalloc(&c->d_counters, 4 * sizeof(unsigned long long))) != hipSuccess) break;
+  } while (0);
+  if (e != hipSuccess) {
+    st = hip_fail(e);
+    rt_context_destroy(c);
+    return st;
+  }
+  *out = c;
+  return RT_OK;
+}
+
+void rt_context_destroy(rt_context *c) {
+  if (!c) return;
+  if (c->device >= 0) (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(c->d_geom);
+  (void)hipFree(c->d_shade);
+  (void)hipFree(c->d_counters);
+  (void)hipFree(c->d_frame);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
+  if (!c || !s || !s->cx || !s->cy || !s->cz || !s->radius || !s->mat_kind || !s->mat_param ||
+      !s->albedo_rgb)
+    return RT_ERR_INVALID;
+  for (uint32_t i = 0; i < s->n; ++i)
+    if (s->mat_kind[i] > RT_DIELECTRIC || s->radius[i] == 0.0f) return RT_ERR_INVALID;
+  const uint32_t n = s->n;
+  const uint32_t n_pad = (n + rtk::kSpherePad - 1) / rtk::kSpherePad * rtk::kSpherePad;
+  const uint32_t n_pairs = n_pad / 2;
+  rtk::pair_geom *geom = new (std::nothrow) rtk::pair_geom[n_pairs ? n_pairs : 1];
+  rtk::shade_rec *shade = new (std::nothrow) rtk::shade_rec[n ? n : 1];
+  if (!geom || !shade) {
+    delete[] geom;
+    delete[] shade;
+    return RT_ERR_NOMEM;
+  }
+  for (uint32_t i = 0; i < n_pad; ++i) {
+    rtk::pair_geom &g = geom[i / 2];
+    const int l = i & 1;
+    if (i < n) {
+      const double x = s->cx[i], y = s->cy[i], z = s->cz[i], r = s->radius[i];
+      g.cx[l] = s->cx[i];
+      g.cy[l] = s->cy[i];
+      g.cz[l] = s->cz[i];
+      // ks = |C|^2 - r^2, in fp64 then rounded once (oracle does the same)
+      g.ks[l] = (float)(x * x + y * y + z * z - r * r);
+    } else {
+      g.cx[l] = g.cy[l] = g.cz[l] = 0.0f;
+      g.ks[l] = __builtin_huge_valf();  // padding: never a candidate
+    }
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    rtk::shade_rec &r = shade[i];
+    std::memset(&r, 0, sizeof r);
+    r.cx = s->cx[i];
+    r.cy = s->cy[i];
+    r.cz = s->cz[i];
+    r.inv_r = 1.0f / s->radius[i];
+    r.ar = s->albedo_rgb[3 * i + 0];
+    r.ag = s->albedo_rgb[3 * i + 1];
+    r.ab = s->albedo_rgb[3 * i + 2];
+    r.param = s->mat_param[i];
+    r.kind = s->mat_kind[i];
+  }
+  int st = RT_OK;
+  hipError_t e = hipSetDevice(c->device);
+  if (e == hipSuccess) {
+    (void)hipFree(c->d_geom);
+    (void)hipFree(c->d_shade);
+    c->d_geom = nullptr;
+    c->d_shade = nullptr;
+    e = hipMalloc(&c->d_geom, sizeof(rtk::pair_geom) * (n_pairs ? n_pairs : 1));
+    if (e == hipSuccess) e = hipMalloc(&c->d_shade, sizeof(rtk::shade_rec) * (n ? n : 1));
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(c->d_geom, geom, sizeof(rtk::pair_geom) * n_pairs, hipMemcpyHostToDevice,
+                         c->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(c->d_shade, shade, sizeof(rtk::shade_rec) * n, hipMemcpyHostToDevice,
+                         c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  }
+  if (e != hipSuccess) st = hip_fail(e);
+  c->n_spheres = st == RT_OK ? n : 0;
+  c->n_pad = st == RT_OK ? n_pad : 0;
+  delete[] geom;
+  delete[] shade;
+  return st;
+}
+
+int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, float *accum_rgb,
+                    void *stream) {
+  if (!c || !cam || !params_ok(prm) || (!accum_rgb && prm->local_rows && prm->width))
+    return RT_ERR_INVALID;
+  if (cam->model != RT_CAMERA_CPU && cam->model != RT_CAMERA_GPU) return RT_ERR_INVALID;
+  if (cam->model == RT_CAMERA_CPU && (prm->width < 2 || prm->height < 2)) return RT_ERR_INVALID;
+  if (!c->d_geom) return RT_ERR_NO_SCENE;
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  RT_HIP(hipSetDevice(c->device));
+  const uint64_t samples = (uint64_t)prm->width * (uint64_t)prm->local_rows * (uint64_t)prm->spp;
+  if (prm->flags & RT_FLAG_KEEP_COUNTERS) {
+    c->last_samples += samples;
+  } else {
+    RT_HIP(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), st));
+    c->last_samples = samples;
+  }
+  if (prm->width == 0 || prm->local_rows == 0) return RT_OK;
+
+  rtk::kparams kp;
+  std::memset(&kp, 0, sizeof kp);
+  kp.cam = *cam;
+  kp.width = prm->width;
+  kp.height = prm->height;
+  kp.spp = prm->spp;
+  kp.max_depth = prm->max_depth;
+  kp.row_block = prm->row_block;
+  kp.band_stride = prm->band_stride;
+  kp.band_offset = prm->band_offset;
+  kp.local_rows = prm->local_rows;
+  kp.tiles_x = (prm->width + rtk::kTile - 1) / rtk::kTile;
+  kp.n_pad = (int)c->n_pad;
+  kp.seed32 = (uint32_t)prm->seed ^ ((uint32_t)(prm->seed >> 32) * 0x9E3779B9u);
+  kp.flags = prm->flags;
+  kp.wm1 = (float)(prm->width - 1);
+  kp.hm1 = (float)(prm->height - 1);
+  const int tiles_y = (prm->local_rows + rtk::kTile - 1) / rtk::kTile;
+  const long long tiles = (long long)kp.tiles_x * tiles_y;
+  const unsigned blocks = (unsigned)((tiles + rtk::kWavesPerBlock - 1) / rtk::kWavesPerBlock);
+  const bool open = prm->flags & RT_FLAG_OPEN_INTERVAL;
+  const bool unitv = prm->flags & RT_FLAG_METAL_UNIT_VECTOR;
+  if (open && unitv)
+    rtk::render_kernel<true, true><<<blocks, rtk::kBlock, 0, st>>>(kp, c->d_geom, c->d_shade,
+                                                                  accum_rgb, c->d_counters);
+  else if (open)
+    rtk::render_kernel<true, false><<<blocks, rtk::kBlock, 0, st>>>(kp, c->d_geom, c->d_shade,
+                                                                   accum_rgb, c->d_counters);
+  else if (unitv)
+    rtk::render_kernel<false, true><<<blocks, rtk::kBlock, 0, st>>>(kp, c->d_geom, c->d_shade,
+                                                                   accum_rgb, c->d_counters);
+  else
+    rtk::render_kernel<false, false><<<blocks, rtk::kBlock, 0, st>>>(kp, c->d_geom, c->d_shade,
+                                                                    accum_rgb, c->d_counters);
+  RT_HIP(hipGetLastError());
+  return RT_OK;
+}
+
+int rt_reset_stats(rt_context *c, void *stream) {
+  if (!c) return RT_ERR_INVALID;
+  RT_HIP(hipSetDevice(c->device));
+  RT_HIP(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long),
+                        stream ? (hipStream_t)stream : c->stream));
+  c->last_samples = 0;
+  return RT_OK;
+}
+
+int rt_collect_stats(rt_context *c, rt_stats *stats) {
+  if (!c || !stats) return RT_ERR_INVALID;
+  unsigned long long h[4] = {0, 0, 0, 0};
+  RT_HIP(hipSetDevice(c->device));
+  RT_HIP(hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
+  stats->segments = h[0];
+  stats->wave_steps = h[1];
+  stats->samples = c->last_samples;
+  stats->sphere_tests = h[0] * (uint64_t)c->n_spheres;
+  stats->kernel_ms = 0.0;
+  return RT_OK;
+}
+
+int rt_render(rt_context *c, const rt_camera *cam, const rt_params *prm, float *host_rgb,
+              rt_stats *stats) {
+  if (!c || !params_ok(prm) || (!host_rgb && prm->local_rows && prm->width)) return RT_ERR_INVALID;
+  const size_t nf = 3 * (size_t)prm->width * (size_t)prm->local_rows;
+  RT_HIP(hipSetDevice(c->device));
+  if (nf > c->frame_floats) {
+    (void)hipFree(c->d_frame);
+    c->d_frame = nullptr;
+    c->frame_floats = 0;
+    RT_HIP(hipMalloc(&c->d_frame, nf * sizeof(float)));
+    c->frame_floats = nf;
+  }
+  RT_HIP(hipEventRecord(c->ev0, c->stream));
+  int st = rt_render_async(c, cam, prm, c->d_frame, c->stream);
+  if (st != RT_OK) return st;
+  RT_HIP(hipEventRecord(c->ev1, c->stream));
+  RT_HIP(hipEventSynchronize(c->ev1));
+  float ms = 0.f;
+  RT_HIP(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  if (nf) RT_HIP(hipMemcpy(host_rgb, c->d_frame, nf * sizeof(float), hipMemcpyDeviceToHost));
+  if (stats) {
+    st = rt_collect_stats(c, stats);
+    if (st != RT_OK) return st;
+    stats->kernel_ms = ms;
+  }
+  return RT_OK;
+}
+
+}  // extern "C"

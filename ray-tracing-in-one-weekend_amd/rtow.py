@@ -1,0 +1,304 @@
+"""rtow -- Python binding (ctypes) of librtow.so, the MI355X render path.
+
+This is the host-side mirror of the reference's process surface for tests,
+bench.py and scripting.  Every call goes straight to the C ABI in
+include/rt.h; there is no Python or CPU fallback for the render itself: if
+librtow.so is missing, or no HIP device is present, the calls raise.
+
+Reference anchors:
+  final_scene()   random_scene()        src/cpu/main.cc:32-76
+  camera_cpu()    camera::camera        src/cpu/camera.h:8-26
+  camera_gpu()    new_camera            src/gpu/camera.h:53-110
+  Context.render  render<<<>>>          src/gpu/camera.h:169-195
+  tonemap()       write_color           src/cpu/color.h:8-23
+  write_ppm()     main.cc:109 / output_image src/gpu/camera.h:197-210
+"""
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librtow.so")
+
+RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC = 0, 1, 2
+RT_CAMERA_CPU, RT_CAMERA_GPU = 0, 1
+RT_FLAG_OPEN_INTERVAL = 1
+RT_FLAG_METAL_UNIT_VECTOR = 2
+RT_FLAG_GPU_SEMANTICS = 3
+RT_FLAG_KEEP_COUNTERS = 1 << 8
+
+_f = ctypes.POINTER(ctypes.c_float)
+_u32 = ctypes.POINTER(ctypes.c_uint32)
+
+
+class SceneView(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint32), ("cx", _f), ("cy", _f), ("cz", _f), ("radius", _f),
+                ("mat_kind", _u32), ("albedo_rgb", _f), ("mat_param", _f)]
+
+
+class SceneBuf(ctypes.Structure):
+    _fields_ = [("capacity", ctypes.c_uint32), ("n", ctypes.c_uint32), ("cx", _f), ("cy", _f),
+                ("cz", _f), ("radius", _f), ("mat_kind", _u32), ("albedo_rgb", _f),
+                ("mat_param", _f)]
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [("model", ctypes.c_int32), ("has_lens", ctypes.c_int32),
+                ("eye", ctypes.c_float * 3), ("corner", ctypes.c_float * 3),
+                ("horiz", ctypes.c_float * 3), ("vert", ctypes.c_float * 3),
+                ("lens_u", ctypes.c_float * 3), ("lens_v", ctypes.c_float * 3)]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("spp", ctypes.c_int32), ("max_depth", ctypes.c_int32),
+                ("seed", ctypes.c_uint64), ("row_block", ctypes.c_int32),
+                ("band_stride", ctypes.c_int32), ("band_offset", ctypes.c_int32),
+                ("local_rows", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("segments", ctypes.c_uint64), ("samples", ctypes.c_uint64),
+                ("sphere_tests", ctypes.c_uint64), ("wave_steps", ctypes.c_uint64),
+                ("kernel_ms", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib():
+    """Load librtow.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; "
+                               "g.build()'` (or make -C ray-tracing-in-one-weekend_amd)")
+        L = ctypes.CDLL(LIB_PATH)
+        d3 = ctypes.POINTER(ctypes.c_double)
+        L.rt_abi_version.restype = ctypes.c_int
+        L.rt_strerror.restype = ctypes.c_char_p
+        L.rt_strerror.argtypes = [ctypes.c_int]
+        L.rt_last_hip_error.restype = ctypes.c_int
+        L.rt_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        L.rt_scene_final.argtypes = [ctypes.c_int, ctypes.POINTER(SceneBuf), d3]
+        L.rt_scene_five.argtypes = [ctypes.POINTER(SceneBuf)]
+        L.rt_camera_cpu.argtypes = [d3, d3, d3, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                    ctypes.c_double, ctypes.POINTER(Camera)]
+        L.rt_camera_gpu.argtypes = [d3, d3, d3, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_double, ctypes.c_double, ctypes.POINTER(Camera)]
+        L.rt_context_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        L.rt_context_destroy.argtypes = [ctypes.c_void_p]
+        L.rt_context_destroy.restype = None
+        L.rt_scene_upload.argtypes = [ctypes.c_void_p, ctypes.POINTER(SceneView)]
+        L.rt_render_async.argtypes = [ctypes.c_void_p, ctypes.POINTER(Camera), ctypes.POINTER(Params),
+                                      ctypes.c_void_p, ctypes.c_void_p]
+        L.rt_render.argtypes = [ctypes.c_void_p, ctypes.POINTER(Camera), ctypes.POINTER(Params),
+                                ctypes.c_void_p, ctypes.POINTER(Stats)]
+        L.rt_collect_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(Stats)]
+        L.rt_reset_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.rt_tonemap_u8.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        L.rt_write_ppm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+class RTError(RuntimeError):
+    def __init__(self, status, where):
+        L = lib()
+        msg = L.rt_strerror(status).decode()
+        if status == -2:
+            msg += f" (hipError {L.rt_last_hip_error()})"
+        super().__init__(f"{where}: {msg} [{status}]")
+        self.status = status
+
+
+def check(status, where):
+    if status != 0:
+        raise RTError(status, where)
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(t)
+
+
+@dataclass
+class Scene:
+    """Sphere scene as SoA numpy arrays (fp32)."""
+    cx: np.ndarray
+    cy: np.ndarray
+    cz: np.ndarray
+    radius: np.ndarray
+    kind: np.ndarray
+    albedo: np.ndarray  # (n, 3)
+    param: np.ndarray
+    rng_next: float = float("nan")
+
+    @property
+    def n(self):
+        return int(self.cx.shape[0])
+
+    def view(self):
+        """A SceneView pointing into this object's arrays (keep self alive)."""
+        for name in ("cx", "cy", "cz", "radius", "albedo", "param"):
+            a = getattr(self, name)
+            if a.dtype != np.float32 or not a.flags.c_contiguous:
+                setattr(self, name, np.ascontiguousarray(a, dtype=np.float32))
+        if self.kind.dtype != np.uint32 or not self.kind.flags.c_contiguous:
+            self.kind = np.ascontiguousarray(self.kind, dtype=np.uint32)
+        return SceneView(self.n, _ptr(self.cx, _f), _ptr(self.cy, _f), _ptr(self.cz, _f),
+                         _ptr(self.radius, _f), _ptr(self.kind, _u32), _ptr(self.albedo, _f),
+                         _ptr(self.param, _f))
+
+
+def _scene_from(fill, capacity):
+    arr = {k: np.zeros(capacity, np.float32) for k in ("cx", "cy", "cz", "radius", "param")}
+    kind = np.zeros(capacity, np.uint32)
+    albedo = np.zeros((capacity, 3), np.float32)
+    buf = SceneBuf(capacity, 0, _ptr(arr["cx"], _f), _ptr(arr["cy"], _f), _ptr(arr["cz"], _f),
+                   _ptr(arr["radius"], _f), _ptr(kind, _u32), _ptr(albedo, _f),
+                   _ptr(arr["param"], _f))
+    nxt = fill(buf)
+    n = buf.n
+    return Scene(arr["cx"][:n].copy(), arr["cy"][:n].copy(), arr["cz"][:n].copy(),
+                 arr["radius"][:n].copy(), kind[:n].copy(), albedo[:n].copy(),
+                 arr["param"][:n].copy(), nxt)
+
+
+def final_scene(half_extent=11):
+    """The final random-spheres scene (486 spheres at half_extent=11)."""
+    cap = (2 * half_extent) ** 2 + 8
+
+    def fill(buf):
+        nxt = ctypes.c_double()
+        check(lib().rt_scene_final(half_extent, ctypes.byref(buf), ctypes.byref(nxt)), "rt_scene_final")
+        return nxt.value
+    return _scene_from(fill, cap)
+
+
+def five_scene():
+    def fill(buf):
+        check(lib().rt_scene_five(ctypes.byref(buf)), "rt_scene_five")
+        return float("nan")
+    return _scene_from(fill, 8)
+
+
+def _d3(v):
+    return (ctypes.c_double * 3)(*[float(x) for x in v])
+
+
+def camera_cpu(lookfrom=(13, 2, 3), lookat=(0, 0, 0), vup=(0, 1, 0), vfov=20.0,
+               aspect=16.0 / 9.0, aperture=0.1, focus_dist=10.0):
+    cam = Camera()
+    check(lib().rt_camera_cpu(_d3(lookfrom), _d3(lookat), _d3(vup), vfov, aspect, aperture,
+                              focus_dist, ctypes.byref(cam)), "rt_camera_cpu")
+    return cam
+
+
+def camera_gpu(width, height, lookfrom=(13, 2, 3), lookat=(0, 0, 0), vup=(0, 1, 0), vfov=20.0,
+               defocus_angle=0.6, focus_dist=10.0):
+    cam = Camera()
+    check(lib().rt_camera_gpu(_d3(lookfrom), _d3(lookat), _d3(vup), vfov, width, height,
+                              defocus_angle, focus_dist, ctypes.byref(cam)), "rt_camera_gpu")
+    return cam
+
+
+def make_params(width, height, spp, max_depth=50, seed=0, flags=0, rank=0, world=1, row_block=8):
+    """Params for rank `rank` of `world` (interleaved row bands of row_block rows)."""
+    if world == 1:
+        return Params(width, height, spp, max_depth, seed, max(1, height), 1, 0, height, flags, 0)
+    band_rows = row_block * world
+    n_bands = -(-height // band_rows)  # every rank gets the same number of bands
+    return Params(width, height, spp, max_depth, seed, row_block, world, rank, n_bands * row_block,
+                  flags, 0)
+
+
+def local_to_global_rows(p):
+    r = np.arange(p.local_rows)
+    band = r // p.row_block
+    return (band * p.band_stride + p.band_offset) * p.row_block + r % p.row_block
+
+
+def device_count():
+    n = ctypes.c_int()
+    check(lib().rt_device_count(ctypes.byref(n)), "rt_device_count")
+    return n.value
+
+
+class Context:
+    """One HIP device + uploaded scene (rt_context)."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        check(lib().rt_context_create(device, ctypes.byref(h)), "rt_context_create")
+        self._h = h
+        self.device = device
+        self.scene = None
+
+    def close(self):
+        if self._h:
+            lib().rt_context_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, scene):
+        v = scene.view()
+        check(lib().rt_scene_upload(self._h, ctypes.byref(v)), "rt_scene_upload")
+        self.scene = scene
+
+    def render(self, cam, params):
+        """Render synchronously; returns (sums float32 [rows, W, 3], Stats)."""
+        out = np.zeros((params.local_rows, params.width, 3), np.float32)
+        st = Stats()
+        check(lib().rt_render(self._h, ctypes.byref(cam), ctypes.byref(params),
+                              out.ctypes.data, ctypes.byref(st)), "rt_render")
+        return out, st
+
+    def render_async(self, cam, params, dev_ptr, stream=0):
+        """Enqueue into a device pointer (e.g. torch tensor.data_ptr()) on a hipStream_t."""
+        check(lib().rt_render_async(self._h, ctypes.byref(cam), ctypes.byref(params),
+                                    ctypes.c_void_p(dev_ptr), ctypes.c_void_p(stream)),
+              "rt_render_async")
+
+    def reset_stats(self, stream=0):
+        check(lib().rt_reset_stats(self._h, ctypes.c_void_p(stream)), "rt_reset_stats")
+
+    def collect_stats(self):
+        st = Stats()
+        check(lib().rt_collect_stats(self._h, ctypes.byref(st)), "rt_collect_stats")
+        return st
+
+
+def tonemap(sums, spp):
+    sums = np.ascontiguousarray(sums, dtype=np.float32)
+    out = np.zeros(sums.shape, np.uint8)
+    n_pix = sums.size // 3
+    check(lib().rt_tonemap_u8(sums.ctypes.data, n_pix, spp, out.ctypes.data), "rt_tonemap_u8")
+    return out
+
+
+def write_ppm(path, rgb, binary=False):
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    h, w = rgb.shape[0], rgb.shape[1]
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    try:
+        check(lib().rt_write_ppm(fd, rgb.ctypes.data, w, h, 1 if binary else 0), "rt_write_ppm")
+    finally:
+        os.close(fd)

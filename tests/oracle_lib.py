@@ -1,0 +1,117 @@
+"""ctypes binding of oracle/librt_oracle.so -- the CHECKER (test infrastructure).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it.
+"""
+import ctypes
+import gzip
+import json
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "librt_oracle.so")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            raise RuntimeError(f"{ORACLE_SO} missing: run `make -C oracle`")
+        L = ctypes.CDLL(ORACLE_SO)
+        L.rto_reference_render.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                                           ctypes.POINTER(ctypes.c_ulonglong)]
+        L.rto_kernel_render.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong),
+                                        ctypes.c_int]
+        L.rto_reference_scene.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                          ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_double)]
+        _lib = L
+    return _lib
+
+
+def reference_render(width, aspect, spp, max_depth=50, scene=0):
+    """fp64 restatement of src/cpu -> (uint8 [H, W, 3] top row first, segments)."""
+    L = lib()
+    h = ctypes.c_int()
+    assert L.rto_reference_render(width, aspect, spp, max_depth, scene, None, ctypes.byref(h), None) == 0
+    out = np.zeros((h.value, width, 3), np.uint8)
+    seg = ctypes.c_ulonglong()
+    assert L.rto_reference_render(width, aspect, spp, max_depth, scene, out.ctypes.data,
+                                  ctypes.byref(h), ctypes.byref(seg)) == 0
+    return out, seg.value
+
+
+def kernel_render(scene, cam, params, threads=0):
+    """fp32 restatement of the kernel algorithm -> (float32 [rows, W, 3], segments)."""
+    import rtow
+    v = scene.view()
+    out = np.zeros((params.local_rows, params.width, 3), np.float32)
+    seg = ctypes.c_ulonglong()
+    assert lib().rto_kernel_render(ctypes.addressof(v), ctypes.addressof(cam), ctypes.addressof(params),
+                                   out.ctypes.data, ctypes.byref(seg), threads) == 0
+    return out, seg.value
+
+
+def reference_scene(half_extent=11):
+    L = lib()
+    n = ctypes.c_size_t()
+    nxt = ctypes.c_double()
+    L.rto_reference_scene(half_extent, None, 0, ctypes.byref(n), None)
+    rows = np.zeros((n.value, 9), np.float64)
+    assert L.rto_reference_scene(half_extent, rows.ctypes.data, n.value, ctypes.byref(n),
+                                 ctypes.byref(nxt)) == 0
+    return rows, nxt.value
+
+
+# ---------------------------------------------------------------- fixtures --
+
+def read_ppm_bytes(data):
+    """Parse P3/P6 bytes -> uint8 [H, W, 3]."""
+    if data[:2] == b"P6":
+        parts = data.split(b"\n", 3)
+        w, h = map(int, parts[1].split())
+        return np.frombuffer(parts[3], np.uint8).reshape(h, w, 3)
+    toks = data.split()
+    assert toks[0] == b"P3"
+    w, h = int(toks[1]), int(toks[2])
+    vals = np.array(toks[4:], dtype=np.int64)
+    return vals.astype(np.uint8).reshape(h, w, 3)
+
+
+def golden_ppm(name):
+    with gzip.open(os.path.join(GOLDEN, name + ".ppm.gz"), "rb") as f:
+        return f.read()
+
+
+def golden_stats():
+    with open(os.path.join(GOLDEN, "ref_stats.json")) as f:
+        return json.load(f)
+
+
+def golden_scene_rows():
+    rows = []
+    for line in open(os.path.join(GOLDEN, "scene_final_gcc.txt")):
+        t = line.split()
+        if t[0] == "next":
+            nxt = float(t[1])
+            continue
+        rows.append([{"L": 0, "M": 1, "D": 2}[t[0]]] + [float(x) for x in t[1:]])
+    return np.array(rows, np.float64), nxt
+
+
+def golden_kat():
+    with open(os.path.join(GOLDEN, "kat.jsonl")) as f:
+        return [json.loads(l) for l in f if l.strip()]
+
+
+def ppm_p3_bytes(rgb):
+    """Format like write_color (src/cpu/color.h:20-22) + header main.cc:109."""
+    h, w = rgb.shape[:2]
+    flat = rgb.reshape(-1, 3)
+    body = "".join("%d %d %d\n" % (r, g, b) for r, g, b in flat)
+    return ("P3\n%d %d\n255\n" % (w, h) + body).encode()

@@ -1,0 +1,145 @@
+"""GPU parity: the HIP kernel (through the C ABI) against the oracle.
+
+* bit-exact vs the kernel-mode CPU restatement on the same seeded inputs
+  (fp32 sums compared with np.array_equal; segment counts equal);
+* statistical vs the reference's own C0 image (north-star bound: image-mean
+  bias <= 1/255 per channel; 16x16 block means within 1.5x the reference's
+  stream-to-stream noise floor);
+* size-independent properties at BASELINE sizes (determinism, partition
+  invariance, sample / segment accounting, finiteness).
+"""
+import numpy as np
+import pytest
+
+from oracle_lib import golden_ppm, golden_stats, kernel_render, read_ppm_bytes
+from test_oracle import stat_compare
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_vs_oracle(rtow, ctx, scene, cam, params):
+    ctx.upload(scene)
+    got, st = ctx.render(cam, params)
+    want, segs = kernel_render(scene, cam, params)
+    return got, st, want, segs
+
+
+def assert_bit_exact(got, st, want, segs):
+    assert np.isfinite(got).all()
+    n_diff = int((got != want).sum())
+    assert n_diff == 0, f"{n_diff} of {got.size} floats differ; max |d| = {np.abs(got - want).max()}"
+    assert st.segments == segs
+
+
+def test_c0_bit_exact_vs_oracle(rtow, gpu_ctx):
+    scene = rtow.final_scene()
+    cam = rtow.camera_cpu(aspect=16.0 / 9.0)
+    p = rtow.make_params(400, 225, 10, seed=0)
+    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p))
+
+
+def test_c0_statistical_vs_reference(rtow, gpu_ctx):
+    scene = rtow.final_scene()
+    gpu_ctx.upload(scene)
+    cam = rtow.camera_cpu(aspect=16.0 / 9.0)
+    sums, st = gpu_ctx.render(cam, rtow.make_params(400, 225, 10, seed=0))
+    img = rtow.tonemap(sums, 10)
+    ref = read_ppm_bytes(golden_ppm("ref_c0_400x225x10"))
+    ref2 = read_ppm_bytes(golden_ppm("ref_c0_shift_400x225x10"))
+    bias, blk, floor = stat_compare(img, ref, ref2)
+    assert np.all(np.abs(bias) <= 1.0), bias
+    assert blk <= 1.5 * floor, (blk, floor)
+    ref_segs = golden_stats()["ref_c0_400x225x10"]["segments"]
+    assert abs(st.segments / ref_segs - 1) < 0.02
+
+
+@pytest.mark.parametrize("flags", [0, 1, 2, 3])
+def test_gpu_camera_and_semantics_bit_exact(rtow, gpu_ctx, flags):
+    """--camera=gpu model (src/gpu/camera.h) and the src/gpu semantic switches."""
+    scene = rtow.final_scene()
+    cam = rtow.camera_gpu(160, 90)
+    p = rtow.make_params(160, 90, 6, seed=1234567890123, flags=flags)
+    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p))
+
+
+def test_five_scene_negative_radius_bit_exact(rtow, gpu_ctx):
+    scene = rtow.five_scene()
+    cam = rtow.camera_cpu(lookfrom=(-2, 2, 1), lookat=(0, 0, -1), aspect=200 / 112,
+                          aperture=0.0, focus_dist=3.4)
+    p = rtow.make_params(200, 112, 16, seed=3)
+    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p))
+
+
+def test_ten_thousand_spheres_bit_exact(rtow, gpu_ctx):
+    scene = rtow.final_scene(half_extent=50)
+    assert 9900 < scene.n <= 10004
+    cam = rtow.camera_cpu(aspect=2.0)
+    p = rtow.make_params(48, 24, 2, seed=11)
+    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p))
+
+
+@pytest.mark.parametrize("w,h,spp,depth", [(13, 7, 3, 50), (8, 8, 1, 1), (65, 9, 2, 2), (1, 2, 4, 50)])
+def test_ragged_and_shallow_bit_exact(rtow, gpu_ctx, w, h, spp, depth):
+    scene = rtow.final_scene()
+    cam = rtow.camera_gpu(w, h) if w < 2 else rtow.camera_cpu(aspect=w / h)
+    p = rtow.make_params(w, h, spp, max_depth=depth, seed=5)
+    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p))
+
+
+def test_spp_zero_and_depth_zero(rtow, gpu_ctx):
+    gpu_ctx.upload(rtow.final_scene())
+    cam = rtow.camera_cpu(aspect=2.0)
+    for p in (rtow.make_params(32, 16, 0), rtow.make_params(32, 16, 4, max_depth=0)):
+        out, st = gpu_ctx.render(cam, p)
+        assert not out.any() and st.segments == 0
+
+
+def test_partition_bit_exact_across_ranks(rtow, gpu_ctx):
+    """Interleaved row bands for G ranks reassemble to the G=1 image exactly."""
+    gpu_ctx.upload(rtow.final_scene())
+    cam = rtow.camera_cpu(aspect=200 / 75)
+    full, st1 = gpu_ctx.render(cam, rtow.make_params(200, 75, 4, seed=9))
+    for world in (2, 8):
+        got = np.zeros_like(full)
+        segs = 0
+        for rank in range(world):
+            p = rtow.make_params(200, 75, 4, seed=9, rank=rank, world=world, row_block=8)
+            tile, st = gpu_ctx.render(cam, p)
+            rows = rtow.local_to_global_rows(p)
+            keep = rows < 75
+            got[rows[keep]] = tile[keep]
+            assert not tile[~keep].any()
+            segs += st.segments
+        assert np.array_equal(got, full)
+        assert segs == st1.segments
+
+
+def test_full_hd_properties(rtow, gpu_ctx):
+    """C1 geometry (1920x1080) at low spp: deterministic, finite, sane accounting."""
+    gpu_ctx.upload(rtow.final_scene())
+    cam = rtow.camera_cpu(aspect=1920 / 1080)
+    p = rtow.make_params(1920, 1080, 4, seed=42)
+    a, st = gpu_ctx.render(cam, p)
+    b, st2 = gpu_ctx.render(cam, p)
+    assert np.array_equal(a, b) and st.segments == st2.segments
+    assert np.isfinite(a).all() and (a >= 0).all()
+    assert st.samples == 1920 * 1080 * 4
+    assert 2.4 < st.segments / st.samples < 3.0
+    # each sample contributes at most 1 per channel (attenuation <= 1, sky <= 1)
+    assert a.max() <= 4.0 + 1e-5
+    # lane efficiency of the path-regeneration loop, for the record
+    eff = st.segments / (64.0 * st.wave_steps)
+    assert 0.3 < eff <= 1.0
+
+
+def test_headline_geometry_one_spp(rtow, gpu_ctx):
+    """3840x2160 (the headline frame) at 1 spp: every pixel written, mean matches
+    the 1920x1080 image statistics (scale invariance of the image mean)."""
+    gpu_ctx.upload(rtow.final_scene())
+    big, st = gpu_ctx.render(rtow.camera_cpu(aspect=3840 / 2160), rtow.make_params(3840, 2160, 1, seed=1))
+    small, _ = gpu_ctx.render(rtow.camera_cpu(aspect=1920 / 1080), rtow.make_params(1920, 1080, 4, seed=2))
+    assert np.isfinite(big).all()
+    assert st.samples == 3840 * 2160
+    m_big = big.reshape(-1, 3).mean(0)
+    m_small = small.reshape(-1, 3).mean(0) / 4
+    assert np.all(np.abs(m_big - m_small) < 0.01), (m_big, m_small)
