@@ -3,9 +3,9 @@
 depth 50 (BASELINE.json `metric`, config 3), on 1..8 MI355X of one node.
 
 One step = one full frame: every rank renders its interleaved row bands
- with the HIP kernel through the C ABI (rt_render_async on torch's
-current stream, device-resident frame tile), then rank 0 gathers the tiles
-with one RCCL gather over xGMI.  Strong scaling: the frame is fixed, N GPUs
+ with the HIP kernel through the C ABI (rt_render_async on a
+dedicated torch stream, device-resident frame tile), then rank 0 gathers the
+tiles with one RCCL gather over xGMI (rtow_dist.py).  Strong scaling: the frame is fixed, N GPUs
 split it.  `value` = closest-hit queries (ray segments) of all ranks per
 second of the max-over-ranks wall time / 1e6.
 
@@ -98,6 +98,7 @@ def main():
     import torch
     import torch.distributed as dist
     import rtow
+    import rtow_dist
 
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
@@ -111,12 +112,13 @@ def main():
     cam = rtow.camera_cpu(aspect=W / H)
     ctx = rtow.Context(local_rank)
     ctx.upload(scene)
-    params = rtow.make_params(W, H, spp, max_depth=a.depth, rank=rank, world=world,
-                              row_block=a.row_block)
+    params = rtow_dist.partition(W, H, spp, world, rank, a.row_block, max_depth=a.depth)
     params.flags |= rtow.RT_FLAG_KEEP_COUNTERS
     tile = torch.zeros((params.local_rows, W, 3), dtype=torch.float32, device=dev)
     gather_list = [torch.empty_like(tile) for _ in range(world)] if (world > 1 and rank == 0) else None
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated stream: the kernel, the HIP events timing it and the RCCL gather
+    # are all ordered on it (torch's default stream would reach the C ABI as NULL)
+    stream = torch.cuda.Stream(dev)
 
     def barrier():
         if world > 1:
@@ -132,21 +134,23 @@ def main():
         if world > 1:
             dist.gather(tile, gather_list, dst=0)
 
-    for i in range(a.warmup):
-        step(1000 + i)
-    torch.cuda.synchronize(dev)
-    ctx.reset_stats(stream.cuda_stream)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(a.steps)]
+    assert stream.cuda_stream != 0
+    with torch.cuda.stream(stream):
+        for i in range(a.warmup):
+            step(1000 + i)
+        torch.cuda.synchronize(dev)
+        ctx.reset_stats(stream.cuda_stream)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(a.steps)]
 
-    barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(i, evs[i])
-    torch.cuda.synchronize(dev)
-    barrier()
-    elapsed = time.perf_counter() - t0
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            step(i, evs[i])
+        torch.cuda.synchronize(dev)
+        barrier()
+        elapsed = time.perf_counter() - t0
 
     st = ctx.collect_stats()
     kernel_ms = [e0.elapsed_time(e1) for e0, e1 in evs]
@@ -165,12 +169,7 @@ def main():
             tiles = torch.stack(gather_list).cpu().numpy()
         else:
             tiles = tile.cpu().numpy()[None]
-        frame = np.zeros((H, W, 3), np.float32)
-        for r in range(world):
-            p = rtow.make_params(W, H, spp, rank=r, world=world, row_block=a.row_block)
-            rows = rtow.local_to_global_rows(p)
-            keep = rows < H
-            frame[rows[keep]] = tiles[r][keep]
+        frame = rtow_dist.assemble(tiles, H, world, a.row_block)
         assert np.isfinite(frame).all() and frame.max() <= spp + 1e-3
         if a.out:
             rtow.write_ppm(a.out, rtow.tonemap(frame, spp), binary=a.out.endswith((".p6", ".pnm")))

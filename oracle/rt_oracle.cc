@@ -340,7 +340,7 @@ void normalize3(float &x, float &y, float &z) {
 }
 
 struct kscene {
-  std::vector<float> cx, cy, cz, ks, inv_r, ar, ag, ab, param;
+  std::vector<float> cx, cy, cz, ks, inv_r, radius, ar, ag, ab, param;
   std::vector<uint32_t> kind;
 };
 
@@ -404,6 +404,7 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
       const float ox2 = -2.0f * o[0], oy2 = -2.0f * o[1], oz2 = -2.0f * o[2];
       float tmax = INFINITY;
       long best = -1;
+      bool near = true;  // which root the winner was taken at
       for (size_t i = 0; i < n; ++i) {
         const float h = fmaf_(sc.cz[i], d[2], fmaf_(sc.cy[i], d[1], fmaf_(sc.cx[i], d[0], nk1)));
         const float g = fmaf_(sc.cz[i], oz2, fmaf_(sc.cy[i], oy2, fmaf_(sc.cx[i], ox2, o2)));
@@ -415,6 +416,7 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
           const bool ok1 = in_range(k.open, t1, 0.001f, tmax);
           if (ok0 || ok1) {
             tmax = ok0 ? t0 : t1;
+            near = ok0;
             best = (long)i;
           }
         }
@@ -428,12 +430,45 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
         break;
       }
       const size_t b = (size_t)best;
+      // refine the winner's chosen root with the better-conditioned forms
+      // (DESIGN.md "Kernel algorithm", step 3)
+      float t = tmax;
+      {
+        const float r2 = sc.radius[b] * sc.radius[b];
+        const float ocx = o[0] - sc.cx[b], ocy = o[1] - sc.cy[b], ocz = o[2] - sc.cz[b];
+        const float bb = dot3(ocx, ocy, ocz, d[0], d[1], d[2]);
+        float cc;
+        if (r2 < o2 + std::fabs(sc.ks[b])) {
+          cc = fmaf_(ocz, ocz, fmaf_(ocy, ocy, fmaf_(ocx, ocx, -r2)));
+        } else {
+          const float g = fmaf_(sc.cz[b], oz2, fmaf_(sc.cy[b], oy2, fmaf_(sc.cx[b], ox2, o2)));
+          cc = g + sc.ks[b];
+        }
+        float disc;
+        if (r2 < bb * bb) {
+          const float fx = fmaf_(-bb, d[0], ocx), fy = fmaf_(-bb, d[1], ocy),
+                      fz = fmaf_(-bb, d[2], ocz);
+          disc = fmaf_(-fz, fz, fmaf_(-fy, fy, fmaf_(-fx, fx, r2)));
+        } else {
+          disc = fmaf_(bb, bb, -cc);
+        }
+        disc = std::fmax(disc, 0.0f);
+        const float sq = std::sqrt(disc);
+        const float q = -(bb + (bb < 0.0f ? -sq : sq));
+        if (q != 0.0f) {
+          const float ta = q, tb = cc / q;
+          const float tr = near ? std::fmin(ta, tb) : std::fmax(ta, tb);
+          if (std::isfinite(tr)) t = tr;
+        }
+      }
       float p[3], nn[3];
-      for (int a = 0; a < 3; ++a) p[a] = fmaf_(tmax, d[a], o[a]);
+      for (int a = 0; a < 3; ++a) p[a] = fmaf_(t, d[a], o[a]);
       nn[0] = (p[0] - sc.cx[b]) * sc.inv_r[b];
       nn[1] = (p[1] - sc.cy[b]) * sc.inv_r[b];
       nn[2] = (p[2] - sc.cz[b]) * sc.inv_r[b];
-      const bool front = dot3(d[0], d[1], d[2], nn[0], nn[1], nn[2]) < 0.0f;
+      // front face from the root taken (exact-arithmetic equivalent of
+      // dot(d, outward) < 0, hittable.h:16-19; outward flips for r < 0)
+      const bool front = near != (sc.inv_r[b] < 0.0f);
       if (!front)
         for (int a = 0; a < 3; ++a) nn[a] = -nn[a];
       const u4 r = pcg4d(pix, sample, (uint32_t)(depth + 1), k.seed32);
@@ -502,6 +537,7 @@ kscene make_kscene(const rt_scene_view &v) {
     s.cz.push_back(v.cz[i]);
     s.ks.push_back((float)(x * x + y * y + z * z - r * r));
     s.inv_r.push_back(1.0f / v.radius[i]);
+    s.radius.push_back(v.radius[i]);
     s.ar.push_back(v.albedo_rgb[3 * i + 0]);
     s.ag.push_back(v.albedo_rgb[3 * i + 1]);
     s.ab.push_back(v.albedo_rgb[3 * i + 2]);

@@ -75,7 +75,9 @@ def test_kernel_algorithm_statistically_matches_reference_c0(rtow):
     assert np.all(np.abs(bias) <= 1.0), bias
     assert blk <= 1.5 * floor, (blk, floor)
     # same amount of work as the reference (segments/sample within 2 %)
-    assert abs(segs / golden_stats()["ref_c0_400x225x10"]["segments"] - 1) < 0.02
+    # (fp64 restatement of the same algorithm: -0.01 %; the winner-root refinement
+    # removes the fp32 self-intersection excess, DESIGN.md "Kernel algorithm")
+    assert abs(segs / golden_stats()["ref_c0_400x225x10"]["segments"] - 1) < 0.003
 
 
 def test_kernel_algorithm_statistically_matches_reference_five_scene(rtow):

@@ -50,7 +50,7 @@ def test_c0_statistical_vs_reference(rtow, gpu_ctx):
     assert np.all(np.abs(bias) <= 1.0), bias
     assert blk <= 1.5 * floor, (blk, floor)
     ref_segs = golden_stats()["ref_c0_400x225x10"]["segments"]
-    assert abs(st.segments / ref_segs - 1) < 0.02
+    assert abs(st.segments / ref_segs - 1) < 0.003
 
 
 @pytest.mark.parametrize("flags", [0, 1, 2, 3])
