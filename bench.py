@@ -33,6 +33,7 @@ sys.path.insert(0, PKG)
 
 PEAK_FP32_TFLOPS = 157.3      # MI355X vector fp32 (MI355X_MICROARCH.md, chip table)
 FLOPS_PER_TEST = 17           # algorithmic flops per ray-sphere test
+FLOPS_PER_BOX = 12            # slab test: 6 fma (2 flop) per ray-box test (BVH mode)
 
 
 def parse():
@@ -46,6 +47,9 @@ def parse():
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--half-extent", type=int, default=11, help="11: 486 spheres; 50: 10k spheres")
     ap.add_argument("--row-block", type=int, default=8)
+    ap.add_argument("--accel", choices=["scan", "bvh"], default="scan",
+                    help="scan: brute-force closest hit (north_star); bvh: wave-uniform BVH walk "
+                         "(bit-identical result, SURVEY 8f-4)")
     ap.add_argument("--cpu-spp", type=int, default=30, help="spp of the bounded CPU sample (400x225)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--out", default="", help="write the gathered frame as PPM (P6 if .pgm/.p6)")
@@ -73,9 +77,10 @@ def cpu_baseline(spp):
             "seconds": round(dt, 3), "sample": sample + " (oracle fp64 restatement)"}
 
 
-def load_traffic(workload):
+def load_traffic(workload, accel="scan"):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json" if accel == "scan"
+                        else f"pmc_traffic_{accel}.json")
     try:
         with open(path) as f:
             d = json.load(f)
@@ -114,6 +119,8 @@ def main():
     ctx.upload(scene)
     params = rtow_dist.partition(W, H, spp, world, rank, a.row_block, max_depth=a.depth)
     params.flags |= rtow.RT_FLAG_KEEP_COUNTERS
+    if a.accel == "bvh":
+        params.flags |= rtow.RT_FLAG_ACCEL_BVH
     tile = torch.zeros((params.local_rows, W, 3), dtype=torch.float32, device=dev)
     gather_list = [torch.empty_like(tile) for _ in range(world)] if (world > 1 and rank == 0) else None
     # a dedicated stream: the kernel, the HIP events timing it and the RCCL gather
@@ -154,6 +161,15 @@ def main():
 
     st = ctx.collect_stats()
     kernel_ms = [e0.elapsed_time(e1) for e0, e1 in evs]
+    # executed work per launch: one instrumented frame (RT_FLAG_COUNT_WORK build),
+    # same seed as timed step 0, outside the timed region
+    wp = rtow_dist.partition(W, H, spp, world, rank, a.row_block, max_depth=a.depth,
+                             flags=(params.flags & ~rtow.RT_FLAG_KEEP_COUNTERS) | rtow.RT_FLAG_COUNT_WORK)
+    wp.seed = 0
+    with torch.cuda.stream(stream):
+        ctx.render_async(cam, wp, tile.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+    work = ctx.collect_stats()
     local = torch.tensor([float(st.segments), float(st.samples), float(st.wave_steps)],
                          dtype=torch.float64, device=dev)
     t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -174,9 +190,10 @@ def main():
         if a.out:
             rtow.write_ppm(a.out, rtow.tonemap(frame, spp), binary=a.out.endswith((".p6", ".pnm")))
 
-        seg_per_launch_rank0 = st.segments / a.steps
         k_avg_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-        achieved = seg_per_launch_rank0 * scene.n * FLOPS_PER_TEST / k_avg_s / 1e12
+        flops = work.sphere_tests * FLOPS_PER_TEST + work.box_tests * FLOPS_PER_BOX
+        achieved = flops / k_avg_s / 1e12
+        bf_achieved = work.bf_tests * FLOPS_PER_TEST / k_avg_s / 1e12
         value = segments / elapsed / 1e6
         out = {
             "metric": "Mray/s (ray segments = closest-hit queries per second), final random-spheres "
@@ -202,11 +219,16 @@ def main():
             "segments_per_frame": int(segments / a.steps),
             "lane_efficiency": round(segments / (64.0 * wave_steps), 4) if wave_steps else None,
             "kernel_ms_avg_rank0": round(k_avg_s * 1e3, 3),
+            "accel": a.accel,
+            "work_per_launch_rank0": {"segments": work.segments, "sphere_tests": work.sphere_tests,
+                                      "box_tests": work.box_tests,
+                                      "brute_force_equiv_tests": work.bf_tests},
             "roofline": {"bound": "valu", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                         "traffic": load_traffic(workload),
-                         "note": "fp32 VALU-bound (no MFMA): 17 flop per ray-sphere test x "
-                                 "spheres x segments per launch / HIP-event kernel time"},
+                         "traffic": load_traffic(workload, a.accel),
+                         "brute_force_equiv_achieved": round(bf_achieved, 2),
+                         "note": "fp32 VALU-bound (no MFMA): executed ray-sphere tests x 17 flop "
+                                 "+ ray-box tests x 12 flop per launch / HIP-event kernel time"},
         }
         if world == 1 and not a.no_cpu_baseline:
             try:

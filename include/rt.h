@@ -57,7 +57,14 @@ enum {
   /* bookkeeping, not semantics: do not zero the context's segment counters
    * before this launch (rt_collect_stats then reports the sum over launches
    * since the last rt_reset_stats) */
-  RT_FLAG_KEEP_COUNTERS = 1u << 8
+  RT_FLAG_KEEP_COUNTERS = 1u << 8,
+  /* acceleration, not semantics: walk a BVH built by rt_scene_upload instead
+   * of scanning every sphere.  Same per-sphere arithmetic and an
+   * order-independent tie rule, so the result is bit-identical to the scan. */
+  RT_FLAG_ACCEL_BVH = 1u << 9,
+  /* count executed ray-sphere and ray-box tests (rt_stats.sphere_tests /
+   * box_tests); selects an instrumented kernel build, for measurement runs */
+  RT_FLAG_COUNT_WORK = 1u << 10
 };
 
 /* Scene as structure-of-arrays; n spheres.  Replaces the device-heap
@@ -123,7 +130,9 @@ typedef struct {
 typedef struct {
   uint64_t segments;     /* closest-hit queries (= hittable_list::hit calls) */
   uint64_t samples;      /* primary samples rendered (width*rows*spp) */
-  uint64_t sphere_tests; /* segments * spheres scanned (brute force) */
+  uint64_t bf_tests;     /* brute-force equivalent ray-sphere tests: segments * spheres */
+  uint64_t sphere_tests; /* executed lane-level ray-sphere tests (RT_FLAG_COUNT_WORK only) */
+  uint64_t box_tests;    /* executed lane-level ray-box tests (RT_FLAG_COUNT_WORK only) */
   uint64_t wave_steps;   /* sum over waves of bounce iterations (lane-efficiency denominator / 64) */
   double kernel_ms;      /* hipEvent time of the render kernel (0 if async) */
 } rt_stats;

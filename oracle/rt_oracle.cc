@@ -380,10 +380,6 @@ void camera_ray(const kctx &k, uint32_t pix, int col, int grow, uint32_t sample,
   normalize3(d[0], d[1], d[2]);
 }
 
-inline bool in_range(bool open, float t, float tmin, float tmax) {
-  return open ? (t > tmin && t < tmax) : (t >= tmin && t <= tmax);
-}
-
 // one pixel, all samples; returns number of closest-hit queries
 unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) {
   const kscene &sc = *k.sc;
@@ -410,13 +406,19 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
         const float g = fmaf_(sc.cz[i], oz2, fmaf_(sc.cy[i], oy2, fmaf_(sc.cx[i], ox2, o2)));
         const float e = fmaf_(h, h, -g);
         if (e >= sc.ks[i]) {
+          // sphere.h:34-44: the root offered is t0 if past t_min, else t1; it
+          // wins if closer than tmax (ties: last index for the closed src/cpu
+          // interval, first for the open src/gpu one -- what a sequential scan
+          // does, stated so that any visiting order gives the same winner)
           const float sq = std::sqrt(e - sc.ks[i]);
           const float t0 = h - sq, t1 = h + sq;
-          const bool ok0 = in_range(k.open, t0, 0.001f, tmax);
-          const bool ok1 = in_range(k.open, t1, 0.001f, tmax);
-          if (ok0 || ok1) {
-            tmax = ok0 ? t0 : t1;
-            near = ok0;
+          const bool use0 = k.open ? t0 > 0.001f : t0 >= 0.001f;
+          const float root = use0 ? t0 : t1;
+          const bool above = k.open ? root > 0.001f : root >= 0.001f;
+          const bool closer = root < tmax || (root == tmax && (k.open ? (long)i < best : (long)i > best));
+          if (above && closer) {
+            tmax = root;
+            near = use0;
             best = (long)i;
           }
         }

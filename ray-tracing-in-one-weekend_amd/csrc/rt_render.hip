@@ -25,9 +25,12 @@
 //    with the CPU restatement in oracle/rt_oracle.cc (kernel mode).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <new>
+#include <vector>
 
 #include "rt.h"
 
@@ -50,6 +53,17 @@ struct __attribute__((aligned(32))) pair_geom {
   f2 cx, cy, cz, ks;  // ks = |C|^2 - r^2
 };
 
+// BVH node for the wave-uniform, stackless traversal (RT_FLAG_ACCEL_BVH): DFS
+// pre-order, one padded AABB per node, `skip` = next node when the subtree is
+// not entered.  32 B = one s_load_dwordx8; the (lo, hi) pairs feed
+// v_pk_fma_f32 like the sphere records do.
+struct __attribute__((aligned(32))) bvh_node {
+  f2 bx, by, bz;  // (lo, hi) per axis
+  int32_t skip;
+  uint32_t leaf;  // 0: internal (first child = this + 1); else 1 + first pair of the leaf
+};
+constexpr int kLeafPairs = 2;  // leaves hold up to 4 spheres, padded to 2 pairs
+
 // per-sphere shading record, fetched once per segment for the closest sphere
 struct __attribute__((aligned(16))) shade_rec {
   float cx, cy, cz, inv_r;
@@ -62,7 +76,7 @@ struct kparams {
   rt_camera cam;
   int width, height, spp, max_depth;
   int row_block, band_stride, band_offset, local_rows;
-  int tiles_x, n_pad;
+  int tiles_x, n_pad, n_nodes;
   uint32_t seed32, flags;
   float wm1, hm1;  // (float)(W-1), (float)(H-1)  (cpu camera model)
 };
@@ -186,20 +200,74 @@ __device__ __forceinline__ bool in_range(float t, float tmin, float tmax) {
   return (t >= tmin) & (t <= tmax);           // src/cpu/sphere.h:38-42
 }
 
-// closest-hit candidate update (sphere.h:34-44 with a = |d|^2 = 1); `near`
-// records which root was taken (entering vs leaving the sphere)
+// running closest hit of one lane (hittable_list::hit's closest_so_far/rec)
+struct hit_state {
+  float tmax;
+  int best;   // original sphere index, -1 = miss
+  bool near;  // the winner was taken at its entering root
+};
+
+// closest-hit candidate update (sphere.h:34-44 with a = |d|^2 = 1).  The root
+// a sphere offers is t0 if t0 is past t_min, else t1; it wins if it is closer
+// than tmax, ties going to the LAST index for src/cpu's closed interval and to
+// the FIRST for src/gpu's open one.  This makes the result independent of the
+// order spheres are visited in: brute-force scan and BVH traversal agree bit
+// for bit.
 template <bool OPEN>
-__device__ __forceinline__ void candidate(bool c, float h, float disc, int idx, float &tmax,
-                                          int &best, bool &near) {
+__device__ __forceinline__ void candidate(bool c, float h, float disc, int idx, hit_state &hs) {
   if (c) {
-    float sq = sqrtf(disc);
-    float t0 = h - sq, t1 = h + sq;
-    bool ok0 = in_range<OPEN>(t0, 0.001f, tmax);
-    bool ok1 = in_range<OPEN>(t1, 0.001f, tmax);
-    if (ok0 | ok1) {
-      tmax = ok0 ? t0 : t1;
-      near = ok0;
-      best = idx;
+    const float sq = sqrtf(disc);
+    const float t0 = h - sq, t1 = h + sq;
+    const bool use0 = OPEN ? (t0 > 0.001f) : (t0 >= 0.001f);
+    const float root = use0 ? t0 : t1;
+    const bool above = OPEN ? (root > 0.001f) : (root >= 0.001f);
+    const bool closer =
+        (root < hs.tmax) | ((root == hs.tmax) & (OPEN ? (idx < hs.best) : (idx > hs.best)));
+    if (above & closer) {
+      hs.tmax = root;
+      hs.best = idx;
+      hs.near = use0;
+    }
+  }
+}
+
+// per-segment ray constants of the expanded quadratic, splatted for packed math
+struct ray_pre {
+  f2 dx, dy, dz, nk1, o2, ox2, oy2, oz2;
+};
+
+// Test NP consecutive sphere pairs (wave-uniform address -> SGPRs).  Per pair:
+// 7 v_pk_fma_f32 + 2 v_cmp; one scalar OR of the ballots decides whether any
+// lane needs the sqrt / interval work.  orig maps slots to original indices
+// (BVH order); nullptr = identity (brute-force order).
+template <bool OPEN, int NP>
+__device__ __forceinline__ void scan_pairs(const pair_geom *__restrict__ g, int slot0,
+                                           const int *__restrict__ orig, const ray_pre &r,
+                                           hit_state &hs) {
+  pair_geom q[NP];
+  f2 h[NP], e[NP];
+  bool c[2 * NP];
+  uint64_t any = 0;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    q[j] = g[j];
+    h[j] = fma2(q[j].cz, r.dz, fma2(q[j].cy, r.dy, fma2(q[j].cx, r.dx, r.nk1)));
+    const f2 gg = fma2(q[j].cz, r.oz2, fma2(q[j].cy, r.oy2, fma2(q[j].cx, r.ox2, r.o2)));
+    e[j] = fma2(h[j], h[j], -gg);
+    // discriminant >= 0  <=>  e >= ks  (exact for finite floats)
+    c[2 * j] = e[j].x >= q[j].ks.x;
+    c[2 * j + 1] = e[j].y >= q[j].ks.y;
+  }
+#pragma unroll
+  for (int j = 0; j < 2 * NP; ++j) any |= __builtin_amdgcn_ballot_w64(c[j]);
+  if (any) {  // wave-uniform: the rare path where some line meets a sphere
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const int s0 = slot0 + 2 * j;
+      const int i0 = orig ? orig[s0] : s0;
+      const int i1 = orig ? orig[s0 + 1] : s0 + 1;
+      candidate<OPEN>(c[2 * j], h[j].x, e[j].x - q[j].ks.x, i0, hs);
+      candidate<OPEN>(c[2 * j + 1], h[j].y, e[j].y - q[j].ks.y, i1, hs);
     }
   }
 }
@@ -246,9 +314,11 @@ __device__ __forceinline__ float refine_root(const shade_rec &sr, float t_scan, 
   return t;
 }
 
-template <bool OPEN, bool METAL_UNIT>
+template <bool OPEN, bool METAL_UNIT, bool BVH, bool STATS>
 __global__ __launch_bounds__(kBlock) void render_kernel(const kparams p,
                                                         const pair_geom *__restrict__ geom,
+                                                        const bvh_node *__restrict__ nodes,
+                                                        const int *__restrict__ orig,
                                                         const shade_rec *__restrict__ shade,
                                                         float *__restrict__ out,
                                                         unsigned long long *__restrict__ counters) {
@@ -269,6 +339,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const kparams p,
   int depth = 0;
   uint32_t sample = 0;
   uint32_t segs = 0, steps = 0;
+  uint32_t lane_tests = 0, lane_boxes = 0;  // executed work, STATS builds only
   bool alive = valid && p.spp > 0 && p.max_depth > 0;  // depth 0: black, no hit test
   if (alive) {
     camera_ray(p, pix, col, grow, 0u, ox, oy, oz, dx, dy, dz);
@@ -284,52 +355,46 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const kparams p,
       const float nk1 = -dot3(ox, oy, oz, dx, dy, dz);
       const float o2 = dot3(ox, oy, oz, ox, oy, oz);
       const float ox2 = -2.0f * ox, oy2 = -2.0f * oy, oz2 = -2.0f * oz;
-      float tmax = __builtin_huge_valf();
-      int best = -1;
-      bool near = true;
-      const f2 vdx = {dx, dx}, vdy = {dy, dy}, vdz = {dz, dz};
-      const f2 vnk1 = {nk1, nk1}, vo2 = {o2, o2};
-      const f2 vox2 = {ox2, ox2}, voy2 = {oy2, oy2}, voz2 = {oz2, oz2};
-      // 8 spheres (4 pairs) per iteration; the pair layout puts (x_i, x_i+1)
-      // in one SGPR pair, so each v_pk_fma_f32 tests two spheres.
-      for (int k = 0; k < n_pairs; k += 4) {
-        const pair_geom q0 = geom[k + 0];
-        const pair_geom q1 = geom[k + 1];
-        const pair_geom q2 = geom[k + 2];
-        const pair_geom q3 = geom[k + 3];
-        const f2 h0 = fma2(q0.cz, vdz, fma2(q0.cy, vdy, fma2(q0.cx, vdx, vnk1)));
-        const f2 h1 = fma2(q1.cz, vdz, fma2(q1.cy, vdy, fma2(q1.cx, vdx, vnk1)));
-        const f2 h2 = fma2(q2.cz, vdz, fma2(q2.cy, vdy, fma2(q2.cx, vdx, vnk1)));
-        const f2 h3 = fma2(q3.cz, vdz, fma2(q3.cy, vdy, fma2(q3.cx, vdx, vnk1)));
-        const f2 g0 = fma2(q0.cz, voz2, fma2(q0.cy, voy2, fma2(q0.cx, vox2, vo2)));
-        const f2 g1 = fma2(q1.cz, voz2, fma2(q1.cy, voy2, fma2(q1.cx, vox2, vo2)));
-        const f2 g2 = fma2(q2.cz, voz2, fma2(q2.cy, voy2, fma2(q2.cx, vox2, vo2)));
-        const f2 g3 = fma2(q3.cz, voz2, fma2(q3.cy, voy2, fma2(q3.cx, vox2, vo2)));
-        const f2 e0 = fma2(h0, h0, -g0);
-        const f2 e1 = fma2(h1, h1, -g1);
-        const f2 e2 = fma2(h2, h2, -g2);
-        const f2 e3 = fma2(h3, h3, -g3);
-        // discriminant >= 0  <=>  e >= ks  (exact for finite floats)
-        const bool c0 = e0.x >= q0.ks.x, c1 = e0.y >= q0.ks.y;
-        const bool c2 = e1.x >= q1.ks.x, c3 = e1.y >= q1.ks.y;
-        const bool c4 = e2.x >= q2.ks.x, c5 = e2.y >= q2.ks.y;
-        const bool c6 = e3.x >= q3.ks.x, c7 = e3.y >= q3.ks.y;
-        const uint64_t any = __builtin_amdgcn_ballot_w64(c0) | __builtin_amdgcn_ballot_w64(c1) |
-                             __builtin_amdgcn_ballot_w64(c2) | __builtin_amdgcn_ballot_w64(c3) |
-                             __builtin_amdgcn_ballot_w64(c4) | __builtin_amdgcn_ballot_w64(c5) |
-                             __builtin_amdgcn_ballot_w64(c6) | __builtin_amdgcn_ballot_w64(c7);
-        if (any) {  // wave-uniform: the rare path where some line meets a sphere
-          const int i = 2 * k;
-          candidate<OPEN>(c0, h0.x, e0.x - q0.ks.x, i + 0, tmax, best, near);
-          candidate<OPEN>(c1, h0.y, e0.y - q0.ks.y, i + 1, tmax, best, near);
-          candidate<OPEN>(c2, h1.x, e1.x - q1.ks.x, i + 2, tmax, best, near);
-          candidate<OPEN>(c3, h1.y, e1.y - q1.ks.y, i + 3, tmax, best, near);
-          candidate<OPEN>(c4, h2.x, e2.x - q2.ks.x, i + 4, tmax, best, near);
-          candidate<OPEN>(c5, h2.y, e2.y - q2.ks.y, i + 5, tmax, best, near);
-          candidate<OPEN>(c6, h3.x, e3.x - q3.ks.x, i + 6, tmax, best, near);
-          candidate<OPEN>(c7, h3.y, e3.y - q3.ks.y, i + 7, tmax, best, near);
+      hit_state hs{__builtin_huge_valf(), -1, true};
+      const ray_pre rp{{dx, dx}, {dy, dy}, {dz, dz}, {nk1, nk1},
+                       {o2, o2}, {ox2, ox2}, {oy2, oy2}, {oz2, oz2}};
+      if (!BVH) {
+        // brute force: 8 spheres (4 pairs) per iteration over the whole array
+        for (int k = 0; k < n_pairs; k += 4) scan_pairs<OPEN, 4>(geom + k, 2 * k, nullptr, rp, hs);
+        if (STATS) lane_tests += 2 * n_pairs;
+      } else {
+        // wave-uniform stackless BVH walk: a node is entered if ANY lane's ray
+        // meets its (conservatively padded) box before that lane's tmax
+        const float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy),
+                    iz = __builtin_amdgcn_rcpf(dz);
+        const f2 vix = {ix, ix}, viy = {iy, iy}, viz = {iz, iz};
+        const f2 vox = {-ox * ix, -ox * ix}, voy = {-oy * iy, -oy * iy}, voz = {-oz * iz, -oz * iz};
+        int node = 0;
+        while (node < p.n_nodes) {
+          const bvh_node nd = nodes[node];
+          const f2 tx = fma2(nd.bx, vix, vox);
+          const f2 ty = fma2(nd.by, viy, voy);
+          const f2 tz = fma2(nd.bz, viz, voz);
+          const float tn = fmaxf(fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y)), 0.0f);
+          const float tf = fminf(fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y)), hs.tmax);
+          if (STATS) ++lane_boxes;
+          if (__builtin_amdgcn_ballot_w64(tn <= tf)) {
+            if (nd.leaf) {
+              const int fp = (int)nd.leaf - 1;
+              scan_pairs<OPEN, kLeafPairs>(geom + fp, 2 * fp, orig, rp, hs);
+              if (STATS) lane_tests += 2 * kLeafPairs;
+              node = nd.skip;
+            } else {
+              node = node + 1;
+            }
+          } else {
+            node = nd.skip;
+          }
         }
       }
+      const float tmax = hs.tmax;
+      const int best = hs.best;
+      const bool near = hs.near;
 
       bool path_done = false;
       if (best < 0) {
@@ -448,11 +513,22 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const kparams p,
   }
   // one atomic per wave for the counters
   uint32_t s = segs;
+  uint64_t lt = lane_tests, lb = lane_boxes;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  for (int off = 32; off > 0; off >>= 1) {
+    s += __shfl_xor(s, off);
+    if (STATS) {
+      lt += __shfl_xor(lt, off);
+      lb += __shfl_xor(lb, off);
+    }
+  }
   if (lane == 0) {
     atomicAdd(&counters[0], (unsigned long long)s);
     atomicAdd(&counters[1], (unsigned long long)steps);
+    if (STATS) {
+      atomicAdd(&counters[2], (unsigned long long)lt);
+      atomicAdd(&counters[3], (unsigned long long)lb);
+    }
   }
 }
 
@@ -463,13 +539,17 @@ struct rt_context {
   int device = -1;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  rtk::pair_geom *d_geom = nullptr;
+  rtk::pair_geom *d_geom = nullptr;      // brute-force order
+  rtk::pair_geom *d_bvh_geom = nullptr;  // BVH leaf order
+  rtk::bvh_node *d_nodes = nullptr;
+  int *d_orig = nullptr;                 // BVH slot -> original index (-1 = padding)
   rtk::shade_rec *d_shade = nullptr;
-  uint32_t n_spheres = 0, n_pad = 0;
+  uint32_t n_spheres = 0, n_pad = 0, n_nodes = 0, n_bvh_slots = 0;
   unsigned long long *d_counters = nullptr;
   float *d_frame = nullptr;
   size_t frame_floats = 0;
   uint64_t last_samples = 0;
+  bool last_stats = false;
 };
 
 namespace {
@@ -490,6 +570,185 @@ bool params_ok(const rt_params *p) {
          p->row_block >= 1 && p->band_stride >= 1 && p->band_offset >= 0 &&
          p->band_offset < p->band_stride && p->local_rows >= 0 &&
          (uint64_t)p->width * (uint64_t)p->height < (1ull << 32);
+}
+
+// ---------------------------------------------------------- BVH build ----
+// Binary BVH over the spheres' boxes, full-sweep SAH on centroids (O(n log^2 n),
+// 10k spheres in a few ms), leaves of <= 4 spheres padded to 2 pairs, nodes in
+// DFS pre-order with skip links for the stackless wave-uniform walk.  Node
+// boxes are padded outward (relative 2e-4 plus nextafter) so the fp32 slab
+// test in the kernel is conservative: a box can be entered needlessly, never
+// skipped wrongly -- the closest hit stays identical to the brute-force scan.
+struct bvh_builder {
+  struct box {
+    double lo[3], hi[3];
+  };
+  std::vector<box> sb;             // per-sphere boxes
+  std::vector<double> cen;         // centroids, 3 per sphere
+  std::vector<uint32_t> ord;       // sphere order being partitioned
+  std::vector<rtk::bvh_node> nodes;
+  std::vector<int> slots;          // slot -> original index, -1 padding
+  static constexpr int kLeaf = 2 * rtk::kLeafPairs;
+
+  static double area(const box &b) {
+    const double dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
+    return dx * dy + dy * dz + dz * dx;
+  }
+  static void grow(box &a, const box &b) {
+    for (int k = 0; k < 3; ++k) {
+      a.lo[k] = std::min(a.lo[k], b.lo[k]);
+      a.hi[k] = std::max(a.hi[k], b.hi[k]);
+    }
+  }
+  static box empty() {
+    box b;
+    for (int k = 0; k < 3; ++k) {
+      b.lo[k] = 1e300;
+      b.hi[k] = -1e300;
+    }
+    return b;
+  }
+  void set_box(rtk::bvh_node &nd, const box &b) {
+    float lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) {
+      const double m = std::max(std::fabs(b.lo[k]), std::fabs(b.hi[k]));
+      const double pad = 2e-4 * (m + (b.hi[k] - b.lo[k])) + 1e-6;
+      lo[k] = std::nextafter((float)(b.lo[k] - pad), -INFINITY);
+      hi[k] = std::nextafter((float)(b.hi[k] + pad), INFINITY);
+    }
+    nd.bx[0] = lo[0];
+    nd.bx[1] = hi[0];
+    nd.by[0] = lo[1];
+    nd.by[1] = hi[1];
+    nd.bz[0] = lo[2];
+    nd.bz[1] = hi[2];
+  }
+  void build(uint32_t b, uint32_t e) {
+    const uint32_t id = (uint32_t)nodes.size();
+    nodes.push_back(rtk::bvh_node{});
+    box all = empty();
+    for (uint32_t i = b; i < e; ++i) grow(all, sb[ord[i]]);
+    const uint32_t n = e - b;
+    if (n <= (uint32_t)kLeaf) {
+      const uint32_t first_slot = (uint32_t)slots.size();
+      for (uint32_t i = b; i < e; ++i) slots.push_back((int)ord[i]);
+      while (slots.size() < first_slot + kLeaf) slots.push_back(-1);
+      rtk::bvh_node &nd = nodes[id];
+      set_box(nd, all);
+      nd.skip = (int32_t)id + 1;
+      nd.leaf = first_slot / 2 + 1;
+      return;
+    }
+    // SAH over the 3 axes, sweeping sorted centroids (ties: original index)
+    double best_cost = 1e300;
+    int best_axis = 0;
+    uint32_t best_split = b + n / 2;
+    std::vector<double> left(n);
+    for (int ax = 0; ax < 3; ++ax) {
+      std::sort(ord.begin() + b, ord.begin() + e, [&](uint32_t x, uint32_t y) {
+        const double cx = cen[3 * x + ax], cy = cen[3 * y + ax];
+        return cx < cy || (cx == cy && x < y);
+      });
+      box acc = empty();
+      for (uint32_t i = 0; i < n; ++i) {
+        grow(acc, sb[ord[b + i]]);
+        left[i] = area(acc);
+      }
+      acc = empty();
+      for (uint32_t i = n - 1; i >= 1; --i) {
+        grow(acc, sb[ord[b + i]]);
+        // split before i: left = [0, i), right = [i, n)
+        const double cost = left[i - 1] * i + area(acc) * (n - i);
+        if (cost < best_cost) {
+          best_cost = cost;
+          best_axis = ax;
+          best_split = b + i;
+        }
+      }
+    }
+    std::sort(ord.begin() + b, ord.begin() + e, [&](uint32_t x, uint32_t y) {
+      const double cx = cen[3 * x + best_axis], cy = cen[3 * y + best_axis];
+      return cx < cy || (cx == cy && x < y);
+    });
+    build(b, best_split);
+    build(best_split, e);
+    rtk::bvh_node &nd = nodes[id];
+    set_box(nd, all);
+    nd.skip = (int32_t)nodes.size();
+    nd.leaf = 0;
+  }
+  void run(const rt_scene_view *s) {
+    const uint32_t n = s->n;
+    sb.resize(n);
+    cen.resize(3 * (size_t)n);
+    ord.resize(n);
+    for (uint32_t i = 0; i < n; ++i) {
+      const double c[3] = {s->cx[i], s->cy[i], s->cz[i]};
+      const double r = std::fabs((double)s->radius[i]);
+      for (int k = 0; k < 3; ++k) {
+        sb[i].lo[k] = c[k] - r;
+        sb[i].hi[k] = c[k] + r;
+        cen[3 * i + k] = c[k];
+      }
+      ord[i] = i;
+    }
+    if (n) build(0, n);
+  }
+};
+
+// scan record of one slot (ks = |C|^2 - r^2 in fp64, rounded once; padding
+// slots have ks = +inf and are never candidates)
+void fill_slot(rtk::pair_geom &g, int l, const rt_scene_view *s, int i) {
+  if (i >= 0) {
+    const double x = s->cx[i], y = s->cy[i], z = s->cz[i], r = s->radius[i];
+    g.cx[l] = s->cx[i];
+    g.cy[l] = s->cy[i];
+    g.cz[l] = s->cz[i];
+    g.ks[l] = (float)(x * x + y * y + z * z - r * r);
+  } else {
+    g.cx[l] = g.cy[l] = g.cz[l] = 0.0f;
+    g.ks[l] = __builtin_huge_valf();
+  }
+}
+
+template <bool O, bool U, bool B, bool S>
+void launch(unsigned blocks, hipStream_t st, const rtk::kparams &kp, rt_context *c, float *out) {
+  rtk::render_kernel<O, U, B, S><<<blocks, rtk::kBlock, 0, st>>>(
+      kp, B ? c->d_bvh_geom : c->d_geom, c->d_nodes, c->d_orig, c->d_shade, out, c->d_counters);
+}
+
+using launch_fn = void (*)(unsigned, hipStream_t, const rtk::kparams &, rt_context *, float *);
+// index: open | unit<<1 | bvh<<2 | stats<<3
+const launch_fn kLaunch[16] = {
+    launch<false, false, false, false>, launch<true, false, false, false>,
+    launch<false, true, false, false>,  launch<true, true, false, false>,
+    launch<false, false, true, false>,  launch<true, false, true, false>,
+    launch<false, true, true, false>,   launch<true, true, true, false>,
+    launch<false, false, false, true>,  launch<true, false, false, true>,
+    launch<false, true, false, true>,   launch<true, true, false, true>,
+    launch<false, false, true, true>,   launch<true, false, true, true>,
+    launch<false, true, true, true>,    launch<true, true, true, true>,
+};
+
+void free_scene(rt_context *c) {
+  (void)hipFree(c->d_geom);
+  (void)hipFree(c->d_bvh_geom);
+  (void)hipFree(c->d_nodes);
+  (void)hipFree(c->d_orig);
+  (void)hipFree(c->d_shade);
+  c->d_geom = c->d_bvh_geom = nullptr;
+  c->d_nodes = nullptr;
+  c->d_orig = nullptr;
+  c->d_shade = nullptr;
+  c->n_spheres = c->n_pad = c->n_nodes = c->n_bvh_slots = 0;
+}
+
+template <class T>
+hipError_t upload_vec(T **dst, const std::vector<T> &v, hipStream_t st) {
+  hipError_t e = hipMalloc(dst, sizeof(T) * (v.empty() ? 1 : v.size()));
+  if (e == hipSuccess && !v.empty())
+    e = hipMemcpyAsync(*dst, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, st);
+  return e;
 }
 
 }  // namespace
@@ -540,8 +799,7 @@ void rt_context_destroy(rt_context *c) {
   if (!c) return;
   if (c->device >= 0) (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  (void)hipFree(c->d_geom);
-  (void)hipFree(c->d_shade);
+  free_scene(c);
   (void)hipFree(c->d_counters);
   (void)hipFree(c->d_frame);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -551,36 +809,17 @@ void rt_context_destroy(rt_context *c) {
 }
 
 int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
-  if (!c || !s || !s->cx || !s->cy || !s->cz || !s->radius || !s->mat_kind || !s->mat_param ||
-      !s->albedo_rgb)
+  if (!c || !s || (s->n && (!s->cx || !s->cy || !s->cz || !s->radius || !s->mat_kind ||
+                            !s->mat_param || !s->albedo_rgb)))
     return RT_ERR_INVALID;
   for (uint32_t i = 0; i < s->n; ++i)
-    if (s->mat_kind[i] > RT_DIELECTRIC || s->radius[i] == 0.0f) return RT_ERR_INVALID;
+    if (s->mat_kind[i] > RT_DIELECTRIC || !(s->radius[i] != 0.0f) || !std::isfinite(s->radius[i]))
+      return RT_ERR_INVALID;
   const uint32_t n = s->n;
   const uint32_t n_pad = (n + rtk::kSpherePad - 1) / rtk::kSpherePad * rtk::kSpherePad;
-  const uint32_t n_pairs = n_pad / 2;
-  rtk::pair_geom *geom = new (std::nothrow) rtk::pair_geom[n_pairs ? n_pairs : 1];
-  rtk::shade_rec *shade = new (std::nothrow) rtk::shade_rec[n ? n : 1];
-  if (!geom || !shade) {
-    delete[] geom;
-    delete[] shade;
-    return RT_ERR_NOMEM;
-  }
-  for (uint32_t i = 0; i < n_pad; ++i) {
-    rtk::pair_geom &g = geom[i / 2];
-    const int l = i & 1;
-    if (i < n) {
-      const double x = s->cx[i], y = s->cy[i], z = s->cz[i], r = s->radius[i];
-      g.cx[l] = s->cx[i];
-      g.cy[l] = s->cy[i];
-      g.cz[l] = s->cz[i];
-      // ks = |C|^2 - r^2, in fp64 then rounded once (oracle does the same)
-      g.ks[l] = (float)(x * x + y * y + z * z - r * r);
-    } else {
-      g.cx[l] = g.cy[l] = g.cz[l] = 0.0f;
-      g.ks[l] = __builtin_huge_valf();  // padding: never a candidate
-    }
-  }
+  std::vector<rtk::pair_geom> geom(n_pad / 2);
+  for (uint32_t i = 0; i < n_pad; ++i) fill_slot(geom[i / 2], i & 1, s, i < n ? (int)i : -1);
+  std::vector<rtk::shade_rec> shade(n);
   for (uint32_t i = 0; i < n; ++i) {
     rtk::shade_rec &r = shade[i];
     std::memset(&r, 0, sizeof r);
@@ -594,34 +833,31 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
     r.param = s->mat_param[i];
     r.kind = s->mat_kind[i];
     r.radius = s->radius[i];
-    {
-      const double x = s->cx[i], y = s->cy[i], z = s->cz[i], rr = s->radius[i];
-      r.ks = (float)(x * x + y * y + z * z - rr * rr);
-    }
+    const double x = s->cx[i], y = s->cy[i], z = s->cz[i], rr = s->radius[i];
+    r.ks = (float)(x * x + y * y + z * z - rr * rr);
   }
-  int st = RT_OK;
-  hipError_t e = hipSetDevice(c->device);
-  if (e == hipSuccess) {
-    (void)hipFree(c->d_geom);
-    (void)hipFree(c->d_shade);
-    c->d_geom = nullptr;
-    c->d_shade = nullptr;
-    e = hipMalloc(&c->d_geom, sizeof(rtk::pair_geom) * (n_pairs ? n_pairs : 1));
-    if (e == hipSuccess) e = hipMalloc(&c->d_shade, sizeof(rtk::shade_rec) * (n ? n : 1));
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(c->d_geom, geom, sizeof(rtk::pair_geom) * n_pairs, hipMemcpyHostToDevice,
-                         c->stream);
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(c->d_shade, shade, sizeof(rtk::shade_rec) * n, hipMemcpyHostToDevice,
-                         c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  bvh_builder bb;
+  bb.run(s);
+  std::vector<rtk::pair_geom> bgeom(bb.slots.size() / 2);
+  for (size_t k = 0; k < bb.slots.size(); ++k) fill_slot(bgeom[k / 2], (int)(k & 1), s, bb.slots[k]);
+
+  RT_HIP(hipSetDevice(c->device));
+  free_scene(c);
+  hipError_t e = upload_vec(&c->d_geom, geom, c->stream);
+  if (e == hipSuccess) e = upload_vec(&c->d_bvh_geom, bgeom, c->stream);
+  if (e == hipSuccess) e = upload_vec(&c->d_nodes, bb.nodes, c->stream);
+  if (e == hipSuccess) e = upload_vec(&c->d_orig, bb.slots, c->stream);
+  if (e == hipSuccess) e = upload_vec(&c->d_shade, shade, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) {
+    free_scene(c);
+    return hip_fail(e);
   }
-  if (e != hipSuccess) st = hip_fail(e);
-  c->n_spheres = st == RT_OK ? n : 0;
-  c->n_pad = st == RT_OK ? n_pad : 0;
-  delete[] geom;
-  delete[] shade;
-  return st;
+  c->n_spheres = n;
+  c->n_pad = n_pad;
+  c->n_nodes = (uint32_t)bb.nodes.size();
+  c->n_bvh_slots = (uint32_t)bb.slots.size();
+  return RT_OK;
 }
 
 int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, float *accum_rgb,
@@ -640,6 +876,7 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
     RT_HIP(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), st));
     c->last_samples = samples;
   }
+  c->last_stats = (prm->flags & RT_FLAG_COUNT_WORK) != 0;
   if (prm->width == 0 || prm->local_rows == 0) return RT_OK;
 
   rtk::kparams kp;
@@ -655,6 +892,7 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
   kp.local_rows = prm->local_rows;
   kp.tiles_x = (prm->width + rtk::kTile - 1) / rtk::kTile;
   kp.n_pad = (int)c->n_pad;
+  kp.n_nodes = (int)c->n_nodes;
   kp.seed32 = (uint32_t)prm->seed ^ ((uint32_t)(prm->seed >> 32) * 0x9E3779B9u);
   kp.flags = prm->flags;
   kp.wm1 = (float)(prm->width - 1);
@@ -662,20 +900,11 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
   const int tiles_y = (prm->local_rows + rtk::kTile - 1) / rtk::kTile;
   const long long tiles = (long long)kp.tiles_x * tiles_y;
   const unsigned blocks = (unsigned)((tiles + rtk::kWavesPerBlock - 1) / rtk::kWavesPerBlock);
-  const bool open = prm->flags & RT_FLAG_OPEN_INTERVAL;
-  const bool unitv = prm->flags & RT_FLAG_METAL_UNIT_VECTOR;
-  if (open && unitv)
-    rtk::render_kernel<true, true><<<blocks, rtk::kBlock, 0, st>>>(kp, c->d_geom, c->d_shade,
-                                                                  accum_rgb, c->d_counters);
-  else if (open)
-    rtk::render_kernel<true, false><<<blocks, rtk::kBlock, 0, st>>>(kp, c->d_geom, c->d_shade,
-                                                                   accum_rgb, c->d_counters);
-  else if (unitv)
-    rtk::render_kernel<false, true><<<blocks, rtk::kBlock, 0, st>>>(kp, c->d_geom, c->d_shade,
-                                                                   accum_rgb, c->d_counters);
-  else
-    rtk::render_kernel<false, false><<<blocks, rtk::kBlock, 0, st>>>(kp, c->d_geom, c->d_shade,
-                                                                    accum_rgb, c->d_counters);
+  const int v = ((prm->flags & RT_FLAG_OPEN_INTERVAL) ? 1 : 0) |
+                ((prm->flags & RT_FLAG_METAL_UNIT_VECTOR) ? 2 : 0) |
+                ((prm->flags & RT_FLAG_ACCEL_BVH) ? 4 : 0) |
+                ((prm->flags & RT_FLAG_COUNT_WORK) ? 8 : 0);
+  kLaunch[v](blocks, st, kp, c, accum_rgb);
   RT_HIP(hipGetLastError());
   return RT_OK;
 }
@@ -697,7 +926,9 @@ int rt_collect_stats(rt_context *c, rt_stats *stats) {
   stats->segments = h[0];
   stats->wave_steps = h[1];
   stats->samples = c->last_samples;
-  stats->sphere_tests = h[0] * (uint64_t)c->n_spheres;
+  stats->bf_tests = h[0] * (uint64_t)c->n_spheres;
+  stats->sphere_tests = c->last_stats ? h[2] : 0;
+  stats->box_tests = c->last_stats ? h[3] : 0;
   stats->kernel_ms = 0.0;
   return RT_OK;
 }

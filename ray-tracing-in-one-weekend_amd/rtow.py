@@ -28,6 +28,8 @@ RT_FLAG_OPEN_INTERVAL = 1
 RT_FLAG_METAL_UNIT_VECTOR = 2
 RT_FLAG_GPU_SEMANTICS = 3
 RT_FLAG_KEEP_COUNTERS = 1 << 8
+RT_FLAG_ACCEL_BVH = 1 << 9
+RT_FLAG_COUNT_WORK = 1 << 10
 
 _f = ctypes.POINTER(ctypes.c_float)
 _u32 = ctypes.POINTER(ctypes.c_uint32)
@@ -62,7 +64,8 @@ class Params(ctypes.Structure):
 
 class Stats(ctypes.Structure):
     _fields_ = [("segments", ctypes.c_uint64), ("samples", ctypes.c_uint64),
-                ("sphere_tests", ctypes.c_uint64), ("wave_steps", ctypes.c_uint64),
+                ("bf_tests", ctypes.c_uint64), ("sphere_tests", ctypes.c_uint64),
+                ("box_tests", ctypes.c_uint64), ("wave_steps", ctypes.c_uint64),
                 ("kernel_ms", ctypes.c_double)]
 
     def as_dict(self):

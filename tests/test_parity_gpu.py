@@ -16,11 +16,20 @@ from test_oracle import stat_compare
 
 pytestmark = pytest.mark.gpu
 
+ACCELS = {"scan": 0, "bvh": 1 << 9}  # RT_FLAG_ACCEL_BVH
 
-def gpu_vs_oracle(rtow, ctx, scene, cam, params):
+
+@pytest.fixture(params=list(ACCELS), ids=list(ACCELS))
+def accel(request):
+    """Both traversal modes must reproduce the brute-force oracle bit for bit."""
+    return ACCELS[request.param]
+
+
+def gpu_vs_oracle(rtow, ctx, scene, cam, params, accel=0):
     ctx.upload(scene)
-    got, st = ctx.render(cam, params)
     want, segs = kernel_render(scene, cam, params)
+    params.flags |= accel
+    got, st = ctx.render(cam, params)
     return got, st, want, segs
 
 
@@ -31,11 +40,11 @@ def assert_bit_exact(got, st, want, segs):
     assert st.segments == segs
 
 
-def test_c0_bit_exact_vs_oracle(rtow, gpu_ctx):
+def test_c0_bit_exact_vs_oracle(rtow, gpu_ctx, accel):
     scene = rtow.final_scene()
     cam = rtow.camera_cpu(aspect=16.0 / 9.0)
     p = rtow.make_params(400, 225, 10, seed=0)
-    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p))
+    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p, accel))
 
 
 def test_c0_statistical_vs_reference(rtow, gpu_ctx):
@@ -54,36 +63,64 @@ def test_c0_statistical_vs_reference(rtow, gpu_ctx):
 
 
 @pytest.mark.parametrize("flags", [0, 1, 2, 3])
-def test_gpu_camera_and_semantics_bit_exact(rtow, gpu_ctx, flags):
+def test_gpu_camera_and_semantics_bit_exact(rtow, gpu_ctx, flags, accel):
     """--camera=gpu model (src/gpu/camera.h) and the src/gpu semantic switches."""
     scene = rtow.final_scene()
     cam = rtow.camera_gpu(160, 90)
     p = rtow.make_params(160, 90, 6, seed=1234567890123, flags=flags)
-    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p))
+    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p, accel))
 
 
-def test_five_scene_negative_radius_bit_exact(rtow, gpu_ctx):
+@pytest.mark.parametrize("flags", [0, 3])
+def test_five_scene_negative_radius_bit_exact(rtow, gpu_ctx, accel, flags):
+    """Duplicate centres (r = 0.5 and -0.4 at one point): exercises the tie rule."""
     scene = rtow.five_scene()
     cam = rtow.camera_cpu(lookfrom=(-2, 2, 1), lookat=(0, 0, -1), aspect=200 / 112,
                           aperture=0.0, focus_dist=3.4)
-    p = rtow.make_params(200, 112, 16, seed=3)
-    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p))
+    p = rtow.make_params(200, 112, 16, seed=3, flags=flags)
+    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p, accel))
 
 
-def test_ten_thousand_spheres_bit_exact(rtow, gpu_ctx):
+def test_ten_thousand_spheres_bit_exact(rtow, gpu_ctx, accel):
     scene = rtow.final_scene(half_extent=50)
     assert 9900 < scene.n <= 10004
     cam = rtow.camera_cpu(aspect=2.0)
     p = rtow.make_params(48, 24, 2, seed=11)
-    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p))
+    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p, accel))
 
 
 @pytest.mark.parametrize("w,h,spp,depth", [(13, 7, 3, 50), (8, 8, 1, 1), (65, 9, 2, 2), (1, 2, 4, 50)])
-def test_ragged_and_shallow_bit_exact(rtow, gpu_ctx, w, h, spp, depth):
+def test_ragged_and_shallow_bit_exact(rtow, gpu_ctx, w, h, spp, depth, accel):
     scene = rtow.final_scene()
     cam = rtow.camera_gpu(w, h) if w < 2 else rtow.camera_cpu(aspect=w / h)
     p = rtow.make_params(w, h, spp, max_depth=depth, seed=5)
-    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p))
+    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p, accel))
+
+
+def test_bvh_equals_scan_at_full_hd(rtow, gpu_ctx):
+    """At BASELINE size (1920x1080, 4 spp) the BVH walk reproduces the scan's
+    fp32 sums exactly, and does fewer ray-sphere tests."""
+    gpu_ctx.upload(rtow.final_scene())
+    cam = rtow.camera_cpu(aspect=1920 / 1080)
+    p = rtow.make_params(1920, 1080, 4, seed=77, flags=1 << 10)
+    a, sa = gpu_ctx.render(cam, p)
+    p.flags |= 1 << 9
+    b, sb = gpu_ctx.render(cam, p)
+    assert np.array_equal(a, b)
+    assert sa.segments == sb.segments
+    assert sa.sphere_tests >= sa.bf_tests  # scan tests every (padded) slot
+    assert sb.sphere_tests < sa.sphere_tests
+    assert sb.box_tests > 0 and sa.box_tests == 0
+
+
+def test_empty_scene_all_sky(rtow, gpu_ctx, accel):
+    s = rtow.final_scene()
+    empty = rtow.Scene(s.cx[:0], s.cy[:0], s.cz[:0], s.radius[:0], s.kind[:0], s.albedo[:0], s.param[:0])
+    cam = rtow.camera_cpu(aspect=2.0)
+    p = rtow.make_params(16, 8, 2, seed=1)
+    got, st, want, segs = gpu_vs_oracle(rtow, gpu_ctx, empty, cam, p, accel)
+    assert_bit_exact(got, st, want, segs)
+    assert st.segments == 16 * 8 * 2
 
 
 def test_spp_zero_and_depth_zero(rtow, gpu_ctx):
