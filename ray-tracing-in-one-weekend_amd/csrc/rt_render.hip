@@ -77,6 +77,7 @@ struct kparams {
   int width, height, spp, max_depth;
   int row_block, band_stride, band_offset, local_rows;
   int tiles_x, n_pad, n_nodes;
+  float oref2;  // BVH padding assumes |ray origin|^2 <= oref2 (else the wave scans)
   uint32_t seed32, flags;
   float wm1, hm1;  // (float)(W-1), (float)(H-1)  (cpu camera model)
 };
@@ -316,6 +317,7 @@ __device__ __forceinline__ float refine_root(const shade_rec &sr, float t_scan, 
 
 template <bool OPEN, bool METAL_UNIT, bool BVH, bool STATS>
 __global__ __launch_bounds__(kBlock) void render_kernel(const kparams p,
+                                                        const pair_geom *__restrict__ scan_geom,
                                                         const pair_geom *__restrict__ geom,
                                                         const bvh_node *__restrict__ nodes,
                                                         const int *__restrict__ orig,
@@ -358,9 +360,12 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const kparams p,
       hit_state hs{__builtin_huge_valf(), -1, true};
       const ray_pre rp{{dx, dx}, {dy, dy}, {dz, dz}, {nk1, nk1},
                        {o2, o2}, {ox2, ox2}, {oy2, oy2}, {oz2, oz2}};
-      if (!BVH) {
+      // the BVH boxes are padded for ray origins within |O| <= oref (see
+      // bvh_builder); a wave-step with any lane beyond that scans everything
+      const bool scan_all = !BVH || __builtin_amdgcn_ballot_w64(o2 > p.oref2) != 0;
+      if (scan_all) {
         // brute force: 8 spheres (4 pairs) per iteration over the whole array
-        for (int k = 0; k < n_pairs; k += 4) scan_pairs<OPEN, 4>(geom + k, 2 * k, nullptr, rp, hs);
+        for (int k = 0; k < n_pairs; k += 4) scan_pairs<OPEN, 4>(scan_geom + k, 2 * k, nullptr, rp, hs);
         if (STATS) lane_tests += 2 * n_pairs;
       } else {
         // wave-uniform stackless BVH walk: a node is entered if ANY lane's ray
@@ -545,6 +550,7 @@ struct rt_context {
   int *d_orig = nullptr;                 // BVH slot -> original index (-1 = padding)
   rtk::shade_rec *d_shade = nullptr;
   uint32_t n_spheres = 0, n_pad = 0, n_nodes = 0, n_bvh_slots = 0;
+  float oref2 = 0.0f;
   unsigned long long *d_counters = nullptr;
   float *d_frame = nullptr;
   size_t frame_floats = 0;
@@ -575,10 +581,17 @@ bool params_ok(const rt_params *p) {
 // ---------------------------------------------------------- BVH build ----
 // Binary BVH over the spheres' boxes, full-sweep SAH on centroids (O(n log^2 n),
 // 10k spheres in a few ms), leaves of <= 4 spheres padded to 2 pairs, nodes in
-// DFS pre-order with skip links for the stackless wave-uniform walk.  Node
-// boxes are padded outward (relative 2e-4 plus nextafter) so the fp32 slab
-// test in the kernel is conservative: a box can be entered needlessly, never
-// skipped wrongly -- the closest hit stays identical to the brute-force scan.
+// DFS pre-order with skip links for the stackless wave-uniform walk.
+//
+// Conservativeness.  The walk must never skip a sphere whose COMPUTED scan
+// root would win, or the result would differ from the brute-force scan.  The
+// scan's hit point P = O + t d satisfies |P - C|^2 = r^2 + (disc_computed -
+// disc_exact), and the expanded quadratic's discriminant error is bounded by
+// ~12 roundings of magnitude (|C| + |O|)^2, i.e. < 2^-19 (|C| + |O|)^2.  So
+// each sphere's box is C +- sqrt(r^2 + 2^-19 (|C| + oref)^2), valid for ray
+// origins |O| <= oref (the kernel scans everything for a wave-step that has
+// any lane beyond oref), and node boxes get a further relative 2^-18 plus an
+// outward fp32 rounding to cover the slab test's own rounding.
 struct bvh_builder {
   struct box {
     double lo[3], hi[3];
@@ -612,7 +625,7 @@ struct bvh_builder {
     float lo[3], hi[3];
     for (int k = 0; k < 3; ++k) {
       const double m = std::max(std::fabs(b.lo[k]), std::fabs(b.hi[k]));
-      const double pad = 2e-4 * (m + (b.hi[k] - b.lo[k])) + 1e-6;
+      const double pad = 0x1p-18 * (m + (b.hi[k] - b.lo[k])) + 1e-6;
       lo[k] = std::nextafter((float)(b.lo[k] - pad), -INFINITY);
       hi[k] = std::nextafter((float)(b.hi[k] + pad), INFINITY);
     }
@@ -677,17 +690,35 @@ struct bvh_builder {
     nd.skip = (int32_t)nodes.size();
     nd.leaf = 0;
   }
+  // oref: the ray-origin bound the padding is valid for -- 64 or 16 beyond the
+  // farthest sphere of radius <= 10, whichever is larger (the huge ground
+  // sphere does not count: rays only start on its visible cap)
+  static double origin_bound(const rt_scene_view *s) {
+    double far = 0.0;
+    for (uint32_t i = 0; i < s->n; ++i) {
+      const double r = std::fabs((double)s->radius[i]);
+      if (r > 10.0) continue;
+      const double c = std::sqrt((double)s->cx[i] * s->cx[i] + (double)s->cy[i] * s->cy[i] +
+                                 (double)s->cz[i] * s->cz[i]);
+      far = std::max(far, c + r);
+    }
+    return std::max(64.0, far + 16.0);
+  }
+  double oref = 64.0;
   void run(const rt_scene_view *s) {
     const uint32_t n = s->n;
+    oref = origin_bound(s);
     sb.resize(n);
     cen.resize(3 * (size_t)n);
     ord.resize(n);
     for (uint32_t i = 0; i < n; ++i) {
       const double c[3] = {s->cx[i], s->cy[i], s->cz[i]};
       const double r = std::fabs((double)s->radius[i]);
+      const double cn = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+      const double reach = std::sqrt(r * r + 0x1p-19 * (cn + oref) * (cn + oref));
       for (int k = 0; k < 3; ++k) {
-        sb[i].lo[k] = c[k] - r;
-        sb[i].hi[k] = c[k] + r;
+        sb[i].lo[k] = c[k] - reach;
+        sb[i].hi[k] = c[k] + reach;
         cen[3 * i + k] = c[k];
       }
       ord[i] = i;
@@ -714,7 +745,7 @@ void fill_slot(rtk::pair_geom &g, int l, const rt_scene_view *s, int i) {
 template <bool O, bool U, bool B, bool S>
 void launch(unsigned blocks, hipStream_t st, const rtk::kparams &kp, rt_context *c, float *out) {
   rtk::render_kernel<O, U, B, S><<<blocks, rtk::kBlock, 0, st>>>(
-      kp, B ? c->d_bvh_geom : c->d_geom, c->d_nodes, c->d_orig, c->d_shade, out, c->d_counters);
+      kp, c->d_geom, c->d_bvh_geom, c->d_nodes, c->d_orig, c->d_shade, out, c->d_counters);
 }
 
 using launch_fn = void (*)(unsigned, hipStream_t, const rtk::kparams &, rt_context *, float *);
@@ -857,6 +888,7 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
   c->n_pad = n_pad;
   c->n_nodes = (uint32_t)bb.nodes.size();
   c->n_bvh_slots = (uint32_t)bb.slots.size();
+  c->oref2 = (float)(0.99 * bb.oref * bb.oref);
   return RT_OK;
 }
 
@@ -893,6 +925,7 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
   kp.tiles_x = (prm->width + rtk::kTile - 1) / rtk::kTile;
   kp.n_pad = (int)c->n_pad;
   kp.n_nodes = (int)c->n_nodes;
+  kp.oref2 = c->oref2;
   kp.seed32 = (uint32_t)prm->seed ^ ((uint32_t)(prm->seed >> 32) * 0x9E3779B9u);
   kp.flags = prm->flags;
   kp.wm1 = (float)(prm->width - 1);
