@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <random>
 #include <thread>
@@ -255,6 +256,11 @@ inline uint8_t tonemap(double v, double scale) {  // color.h:8-23
 
 inline float fmaf_(float a, float b, float c) { return std::fmaf(a, b, c); }
 
+// debug tracing of one sample (rto_trace): prints every segment and every
+// candidate sphere (root, discriminant) -- test tooling only
+FILE *g_trace = nullptr;
+long g_trace_sample = -1;
+
 struct u4 {
   uint32_t x, y, z, w;
 };
@@ -401,6 +407,10 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
       float tmax = INFINITY;
       long best = -1;
       bool near = true;  // which root the winner was taken at
+      const bool tr = g_trace && (long)sample == g_trace_sample;
+      if (tr)
+        std::fprintf(g_trace, "seg %d O=(%.9g %.9g %.9g) D=(%.9g %.9g %.9g) |O|^2=%.9g\n", depth, o[0],
+                     o[1], o[2], d[0], d[1], d[2], o2);
       for (size_t i = 0; i < n; ++i) {
         const float h = fmaf_(sc.cz[i], d[2], fmaf_(sc.cy[i], d[1], fmaf_(sc.cx[i], d[0], nk1)));
         const float g = fmaf_(sc.cz[i], oz2, fmaf_(sc.cy[i], oy2, fmaf_(sc.cx[i], ox2, o2)));
@@ -416,6 +426,9 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
           const float root = use0 ? t0 : t1;
           const bool above = k.open ? root > 0.001f : root >= 0.001f;
           const bool closer = root < tmax || (root == tmax && (k.open ? (long)i < best : (long)i > best));
+          if (tr)
+            std::fprintf(g_trace, "   cand %zu disc=%.9g t0=%.9g t1=%.9g root=%.9g above=%d closer=%d\n", i,
+                         e - sc.ks[i], t0, t1, root, (int)above, (int)closer);
           if (above && closer) {
             tmax = root;
             near = use0;
@@ -423,6 +436,7 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
           }
         }
       }
+      if (tr) std::fprintf(g_trace, "  -> best %ld t %.9g near %d\n", best, tmax, (int)near);
       if (best < 0) {  // sky, main.cc:27-29
         const float a = 0.5f * (d[1] + 1.0f);
         const float s0 = 1.0f - a;
@@ -641,6 +655,22 @@ int rto_kernel_render(const rt_scene_view *scene, const rt_camera *cam, const rt
   worker();
   for (auto &t : pool) t.join();
   if (segments) *segments = total.load();
+  return 0;
+}
+
+int rto_trace(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p, int col,
+              int grow, long sample) {
+  if (!scene || !cam || !p) return -1;
+  const kscene sc = make_kscene(*scene);
+  kctx k{&sc, cam, p, (uint32_t)p->seed ^ ((uint32_t)(p->seed >> 32) * 0x9E3779B9u),
+         (p->flags & RT_FLAG_OPEN_INTERVAL) != 0, (p->flags & RT_FLAG_METAL_UNIT_VECTOR) != 0};
+  g_trace = stdout;
+  g_trace_sample = sample;
+  float acc[3];
+  kernel_pixel(k, col, grow, acc);
+  std::fflush(stdout);
+  g_trace = nullptr;
+  g_trace_sample = -1;
   return 0;
 }
 

@@ -18,6 +18,9 @@ int rto_reference_render(int width, double aspect, int spp, int max_depth, int s
 int rto_kernel_render(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
                       float *out, unsigned long long *segments, int threads);
 /* fp64 final scene rows: kind, cx, cy, cz, r, albedo rgb, param (9 doubles). */
+/* debug: print one sample's segments and candidates to stdout */
+int rto_trace(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p, int col,
+              int grow, long sample);
 int rto_reference_scene(int half_extent, double *rows, size_t capacity, size_t *n_out,
                         double *rng_next);
 #ifdef __cplusplus

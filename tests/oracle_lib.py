@@ -57,6 +57,17 @@ def kernel_render(scene, cam, params, threads=0):
     return out, seg.value
 
 
+def trace(scene, cam, params, col, row, sample, max_depth=50):
+    """Print one sample's segments and candidate spheres (debug tooling)."""
+    import copy
+    v = scene.view()
+    p = copy.copy(params)
+    p.max_depth = max_depth
+    lib().rto_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                ctypes.c_int, ctypes.c_long]
+    lib().rto_trace(ctypes.addressof(v), ctypes.addressof(cam), ctypes.addressof(p), col, row, sample)
+
+
 def reference_scene(half_extent=11):
     L = lib()
     n = ctypes.c_size_t()
