@@ -370,8 +370,14 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const kparams p,
       } else {
         // wave-uniform stackless BVH walk: a node is entered if ANY lane's ray
         // meets its (conservatively padded) box before that lane's tmax
-        const float ix = __builtin_amdgcn_rcpf(dx), iy = __builtin_amdgcn_rcpf(dy),
-                    iz = __builtin_amdgcn_rcpf(dz);
+        // |d| components are clamped away from 0 before the reciprocal: an
+        // exactly axis-parallel ray (it happens ~20 times per 4K frame) would
+        // otherwise give slab bounds (-inf, inf - inf = NaN), and IEEE min/max
+        // then return -inf, culling a box the ray is inside.  With the clamp
+        // every slab value is finite; the ray bends by < 1e-14 over any length.
+        const float ix = __builtin_amdgcn_rcpf(fabsf(dx) < 1e-18f ? copysignf(1e-18f, dx) : dx);
+        const float iy = __builtin_amdgcn_rcpf(fabsf(dy) < 1e-18f ? copysignf(1e-18f, dy) : dy);
+        const float iz = __builtin_amdgcn_rcpf(fabsf(dz) < 1e-18f ? copysignf(1e-18f, dz) : dz);
         const f2 vix = {ix, ix}, viy = {iy, iy}, viz = {iz, iz};
         const f2 vox = {-ox * ix, -ox * ix}, voy = {-oy * iy, -oy * iy}, voz = {-oz * iz, -oz * iz};
         int node = 0;
