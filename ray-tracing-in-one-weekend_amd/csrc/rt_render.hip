@@ -380,9 +380,16 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const kparams p,
         const float iz = __builtin_amdgcn_rcpf(fabsf(dz) < 1e-18f ? copysignf(1e-18f, dz) : dz);
         const f2 vix = {ix, ix}, viy = {iy, iy}, viz = {iz, iz};
         const f2 vox = {-ox * ix, -ox * ix}, voy = {-oy * iy, -oy * iy}, voz = {-oz * iz, -oz * iz};
+        // the wave walks the DFS order of its majority direction octant, so
+        // coherent rays visit near children first and tmax culls the rest
+        const uint32_t half = __builtin_popcountll(__builtin_amdgcn_ballot_w64(true)) / 2;
+        const int oct = (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dx < 0.0f)) > half ? 1 : 0) |
+                        (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dy < 0.0f)) > half ? 2 : 0) |
+                        (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dz < 0.0f)) > half ? 4 : 0);
+        const bvh_node *__restrict__ order = nodes + (size_t)oct * p.n_nodes;
         int node = 0;
         while (node < p.n_nodes) {
-          const bvh_node nd = nodes[node];
+          const bvh_node nd = order[node];
           const f2 tx = fma2(nd.bx, vix, vox);
           const f2 ty = fma2(nd.by, viy, voy);
           const f2 tz = fma2(nd.bz, viz, voz);
@@ -642,21 +649,28 @@ struct bvh_builder {
     nd.bz[0] = lo[2];
     nd.bz[1] = hi[2];
   }
-  void build(uint32_t b, uint32_t e) {
-    const uint32_t id = (uint32_t)nodes.size();
-    nodes.push_back(rtk::bvh_node{});
+  // tree in memory; emitted afterwards in 8 DFS orders (one per direction
+  // octant, near child first along the node's split axis)
+  struct tnode {
+    box b;
+    int axis = 0;
+    int left = -1, right = -1;
+    uint32_t leaf = 0;  // 1 + first pair, or 0
+  };
+  std::vector<tnode> tree;
+  int build(uint32_t b, uint32_t e) {
+    const int id = (int)tree.size();
+    tree.push_back(tnode{});
     box all = empty();
     for (uint32_t i = b; i < e; ++i) grow(all, sb[ord[i]]);
+    tree[id].b = all;
     const uint32_t n = e - b;
     if (n <= (uint32_t)kLeaf) {
       const uint32_t first_slot = (uint32_t)slots.size();
       for (uint32_t i = b; i < e; ++i) slots.push_back((int)ord[i]);
       while (slots.size() < first_slot + kLeaf) slots.push_back(-1);
-      rtk::bvh_node &nd = nodes[id];
-      set_box(nd, all);
-      nd.skip = (int32_t)id + 1;
-      nd.leaf = first_slot / 2 + 1;
-      return;
+      tree[id].leaf = first_slot / 2 + 1;
+      return id;
     }
     // SAH over the 3 axes, sweeping sorted centroids (ties: original index)
     double best_cost = 1e300;
@@ -689,13 +703,35 @@ struct bvh_builder {
       const double cx = cen[3 * x + best_axis], cy = cen[3 * y + best_axis];
       return cx < cy || (cx == cy && x < y);
     });
-    build(b, best_split);
-    build(best_split, e);
+    const int l = build(b, best_split);
+    const int r = build(best_split, e);
+    tree[id].axis = best_axis;
+    tree[id].left = l;
+    tree[id].right = r;
+    return id;
+  }
+  // DFS pre-order for octant oct (bit k set = direction negative along axis k):
+  // a ray moving towards -axis meets the upper (right) child first
+  void emit(int t, int oct, size_t base) {
+    const size_t id = nodes.size();
+    nodes.push_back(rtk::bvh_node{});
+    const tnode &tn = tree[t];
+    if (tn.leaf) {
+      rtk::bvh_node &nd = nodes[id];
+      set_box(nd, tn.b);
+      nd.skip = (int32_t)(id + 1 - base);
+      nd.leaf = tn.leaf;
+      return;
+    }
+    const bool neg = (oct >> tn.axis) & 1;
+    emit(neg ? tn.right : tn.left, oct, base);
+    emit(neg ? tn.left : tn.right, oct, base);
     rtk::bvh_node &nd = nodes[id];
-    set_box(nd, all);
-    nd.skip = (int32_t)nodes.size();
+    set_box(nd, tn.b);
+    nd.skip = (int32_t)(nodes.size() - base);
     nd.leaf = 0;
   }
+  size_t per_order = 0;
   // oref: the ray-origin bound the padding is valid for -- 64 or 16 beyond the
   // farthest sphere of radius <= 10, whichever is larger (the huge ground
   // sphere does not count: rays only start on its visible cap)
@@ -729,7 +765,10 @@ struct bvh_builder {
       }
       ord[i] = i;
     }
-    if (n) build(0, n);
+    if (!n) return;
+    build(0, n);
+    for (int oct = 0; oct < 8; ++oct) emit(0, oct, nodes.size());
+    per_order = nodes.size() / 8;
   }
 };
 
@@ -892,7 +931,7 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
   }
   c->n_spheres = n;
   c->n_pad = n_pad;
-  c->n_nodes = (uint32_t)bb.nodes.size();
+  c->n_nodes = (uint32_t)bb.per_order;  // nodes holds 8 orders of this many
   c->n_bvh_slots = (uint32_t)bb.slots.size();
   c->oref2 = (float)(0.99 * bb.oref * bb.oref);
   return RT_OK;
