@@ -312,17 +312,17 @@ void sincos_turn(float u, float &s, float &c) {
   c = ((q + 1) & 2) ? -c0 : c0;
 }
 
+// u^(1/3) without division: inverse-cube-root seed + 4 Newton steps, u * y^2
 float cbrt01(float u) {
   uint32_t i;
   std::memcpy(&i, &u, 4);
-  i = i / 3u + 709921077u;
+  i = 0x54a2fa8cu - i / 3u;
   float y;
   std::memcpy(&y, &i, 4);
-  for (int k = 0; k < 3; ++k) {
-    float y2 = y * y;
-    y = fmaf_(y, 0.666666687f, (u / y2) * 0.333333343f);
-  }
-  return u == 0.0f ? 0.0f : y;
+  const float u3 = u * 0.333333343f;
+  for (int k = 0; k < 4; ++k) y = y * fmaf_(-u3, (y * y) * y, 1.33333337f);
+  const float c = u * (y * y);
+  return u == 0.0f ? 0.0f : c;
 }
 
 void unit_vec(float u1, float u2, float &x, float &y, float &z) {
@@ -346,7 +346,7 @@ void normalize3(float &x, float &y, float &z) {
 }
 
 struct kscene {
-  std::vector<float> cx, cy, cz, ks, inv_r, radius, ar, ag, ab, param;
+  std::vector<float> cx, cy, cz, ks, inv_r, radius, ar, ag, ab, param, inv_param, r0;
   std::vector<uint32_t> kind;
 };
 
@@ -366,8 +366,9 @@ void camera_ray(const kctx &k, uint32_t pix, int col, int grow, uint32_t sample,
   float fs, ft;
   if (c.model == RT_CAMERA_CPU) {
     int j = k.p->height - 1 - grow;
-    fs = ((float)col + u1) / (float)(k.p->width - 1);
-    ft = ((float)j + u2) / (float)(k.p->height - 1);
+    // 1/(W-1) and 1/(H-1) rounded once to fp32 (main.cc:116-117 divides)
+    fs = ((float)col + u1) * (float)(1.0 / (k.p->width - 1));
+    ft = ((float)j + u2) * (float)(1.0 / (k.p->height - 1));
   } else {
     fs = (float)col + (u1 - 0.5f);
     ft = (float)grow + (u2 - 0.5f);
@@ -513,12 +514,11 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
         th[1] *= sc.ag[b];
         th[2] *= sc.ab[b];
       } else {
-        const float ratio = front ? 1.0f / sc.param[b] : sc.param[b];
+        const float ratio = front ? sc.inv_param[b] : sc.param[b];
         const float cos_t = std::fmin(-dot3(d[0], d[1], d[2], nn[0], nn[1], nn[2]), 1.0f);
         const float sin_t = std::sqrt(fmaf_(-cos_t, cos_t, 1.0f));
         const bool cannot = ratio * sin_t > 1.0f;
-        float r0 = (1.0f - ratio) / (1.0f + ratio);
-        r0 = r0 * r0;
+        const float r0 = sc.r0[b];  // ((1-ior)/(1+ior))^2, same for ior and 1/ior
         const float x = 1.0f - cos_t;
         const float x2 = x * x;
         const float refl = fmaf_(1.0f - r0, x2 * x2 * x, r0);
@@ -558,6 +558,10 @@ kscene make_kscene(const rt_scene_view &v) {
     s.ag.push_back(v.albedo_rgb[3 * i + 1]);
     s.ab.push_back(v.albedo_rgb[3 * i + 2]);
     s.param.push_back(v.mat_param[i]);
+    const double ior = v.mat_param[i];
+    s.inv_param.push_back((float)(1.0 / ior));
+    const double r0 = (1.0 - ior) / (1.0 + ior);
+    s.r0.push_back((float)(r0 * r0));
     s.kind.push_back(v.mat_kind[i]);
   }
   return s;

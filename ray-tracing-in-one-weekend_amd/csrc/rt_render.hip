@@ -67,9 +67,12 @@ constexpr int kLeafPairs = 2;  // leaves hold up to 4 spheres, padded to 2 pairs
 // per-sphere shading record, fetched once per segment for the closest sphere
 struct __attribute__((aligned(16))) shade_rec {
   float cx, cy, cz, inv_r;
-  float ar, ag, ab, param;
+  float ar, ag, ab, param;  // albedo (1,1,1 for dielectrics); fuzz | ior
   uint32_t kind;
-  float radius, ks, pad;
+  float radius, ks;
+  float inv_param;          // 1/ior (dielectric)
+  float r0;                 // Schlick r0 = ((1-ior)/(1+ior))^2 (dielectric)
+  float pad0, pad1, pad2;
 };
 
 struct kparams {
@@ -79,7 +82,7 @@ struct kparams {
   int tiles_x, n_pad, n_nodes;
   float oref2;  // BVH padding assumes |ray origin|^2 <= oref2 (else the wave scans)
   uint32_t seed32, flags;
-  float wm1, hm1;  // (float)(W-1), (float)(H-1)  (cpu camera model)
+  float inv_wm1, inv_hm1;  // 1/(W-1), 1/(H-1) rounded once (cpu camera model)
 };
 
 // ---------------------------------------------------------------- RNG ----
@@ -123,16 +126,17 @@ __device__ __forceinline__ void sincos_turn(float u, float &s, float &c) {
   c = ((q + 1) & 2) ? -c0 : c0;
 }
 
-// cube root of u in [0,1): bit-hack seed + 3 Newton steps (same ops on host).
+// cube root of u in [0,1) without a division: inverse-cube-root seed from the
+// exponent bits, 4 Newton steps y <- y (4/3 - (u/3) y^3), then u * y^2.  Same
+// ops on the host restatement.  (Replaces the rejection loop's radius law of
+// random_in_unit_sphere, vec3.h:105-112: |p| = u^(1/3) for a uniform ball.)
 __device__ __forceinline__ float cbrt01(float u) {
-  uint32_t i = __float_as_uint(u) / 3u + 709921077u;
-  float y = __uint_as_float(i);
+  float y = __uint_as_float(0x54a2fa8cu - __float_as_uint(u) / 3u);
+  const float u3 = u * 0.333333343f;
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    float y2 = y * y;
-    y = fmaf(y, 0.666666687f, (u / y2) * 0.333333343f);
-  }
-  return u == 0.0f ? 0.0f : y;
+  for (int k = 0; k < 4; ++k) y = y * fmaf(-u3, (y * y) * y, 1.33333337f);
+  const float c = u * (y * y);
+  return u == 0.0f ? 0.0f : c;
 }
 
 // uniform direction on the unit sphere (replaces the rejection loop of
@@ -168,8 +172,8 @@ __device__ __forceinline__ void camera_ray(const kparams &p, uint32_t pix, int c
   float fs, ft;
   if (p.cam.model == RT_CAMERA_CPU) {
     int j = p.height - 1 - grow;
-    fs = ((float)col + u1) / p.wm1;
-    ft = ((float)j + u2) / p.hm1;
+    fs = ((float)col + u1) * p.inv_wm1;
+    ft = ((float)j + u2) * p.inv_hm1;
   } else {
     fs = (float)col + (u1 - 0.5f);
     ft = (float)grow + (u2 - 0.5f);
@@ -438,12 +442,17 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const kparams p,
           nz = -nz;
         }
         const uint4 r = pcg4d(pix, sample - 1u, (uint32_t)(depth + 1), p.seed32);
+        // shared by the material branches (computed once: lanes of one wave
+        // usually hit several materials, so the branches all execute)
+        const float dn = dot3(dx, dy, dz, nx, ny, nz);
+        const float k2 = -2.0f * dn;  // reflect(d, n) = d - 2 (d.n) n, vec3.h:122
+        const float rx = fmaf(k2, nx, dx), ry = fmaf(k2, ny, dy), rz = fmaf(k2, nz, dz);
+        float ux, uy, uz;
+        unit_vec(unif(r.x), unif(r.y), ux, uy, uz);
         float sx, sy, sz;
         bool scattered = true;
         if (sr.kind == RT_LAMBERTIAN) {
           // material.h:19-30
-          float ux, uy, uz;
-          unit_vec(unif(r.x), unif(r.y), ux, uy, uz);
           sx = nx + ux;
           sy = ny + uy;
           sz = nz + uz;
@@ -453,40 +462,27 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const kparams p,
             sy = ny;
             sz = nz;
           }
-          thr *= sr.ar;
-          thg *= sr.ag;
-          thb *= sr.ab;
         } else if (sr.kind == RT_METAL) {
           // material.h:40-46
-          const float k = -2.0f * dot3(dx, dy, dz, nx, ny, nz);
-          const float rx = fmaf(k, nx, dx), ry = fmaf(k, ny, dy), rz = fmaf(k, nz, dz);
-          float ux, uy, uz;
-          unit_vec(unif(r.x), unif(r.y), ux, uy, uz);
           float fz = sr.param;
           if (!METAL_UNIT) fz *= cbrt01(unif(r.z));  // random_in_unit_sphere
           sx = fmaf(fz, ux, rx);
           sy = fmaf(fz, uy, ry);
           sz = fmaf(fz, uz, rz);
           scattered = dot3(sx, sy, sz, nx, ny, nz) > 0.0f;
-          thr *= sr.ar;
-          thg *= sr.ag;
-          thb *= sr.ab;
         } else {
-          // dielectric, material.h:57-87
-          const float ratio = front ? 1.0f / sr.param : sr.param;
-          const float cos_t = fminf(-dot3(dx, dy, dz, nx, ny, nz), 1.0f);
+          // dielectric, material.h:57-87 (r0 is the same for ior and 1/ior)
+          const float ratio = front ? sr.inv_param : sr.param;
+          const float cos_t = fminf(-dn, 1.0f);
           const float sin_t = sqrtf(fmaf(-cos_t, cos_t, 1.0f));
           const bool cannot = ratio * sin_t > 1.0f;
-          float r0 = (1.0f - ratio) / (1.0f + ratio);
-          r0 = r0 * r0;
           const float x = 1.0f - cos_t;
           const float x2 = x * x;
-          const float refl = fmaf(1.0f - r0, x2 * x2 * x, r0);
+          const float refl = fmaf(1.0f - sr.r0, x2 * x2 * x, sr.r0);
           if (cannot || refl > unif(r.x)) {
-            const float k = -2.0f * dot3(dx, dy, dz, nx, ny, nz);
-            sx = fmaf(k, nx, dx);
-            sy = fmaf(k, ny, dy);
-            sz = fmaf(k, nz, dz);
+            sx = rx;
+            sy = ry;
+            sz = rz;
           } else {
             const float qx = ratio * fmaf(cos_t, nx, dx);
             const float qy = ratio * fmaf(cos_t, ny, dy);
@@ -497,6 +493,10 @@ __global__ __launch_bounds__(kBlock) void render_kernel(const kparams p,
             sz = fmaf(m, nz, qz);
           }
         }
+        // attenuation = albedo (dielectrics store 1,1,1: the product is exact)
+        thr *= sr.ar;
+        thg *= sr.ag;
+        thb *= sr.ab;
         ++depth;
         if (!scattered || depth >= p.max_depth) {
           path_done = true;  // absorbed, or bounce limit (main.cc:16-17): black
@@ -903,14 +903,19 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
     r.cy = s->cy[i];
     r.cz = s->cz[i];
     r.inv_r = 1.0f / s->radius[i];
-    r.ar = s->albedo_rgb[3 * i + 0];
-    r.ag = s->albedo_rgb[3 * i + 1];
-    r.ab = s->albedo_rgb[3 * i + 2];
+    const bool glass = s->mat_kind[i] == RT_DIELECTRIC;
+    r.ar = glass ? 1.0f : s->albedo_rgb[3 * i + 0];
+    r.ag = glass ? 1.0f : s->albedo_rgb[3 * i + 1];
+    r.ab = glass ? 1.0f : s->albedo_rgb[3 * i + 2];
     r.param = s->mat_param[i];
     r.kind = s->mat_kind[i];
     r.radius = s->radius[i];
     const double x = s->cx[i], y = s->cy[i], z = s->cz[i], rr = s->radius[i];
     r.ks = (float)(x * x + y * y + z * z - rr * rr);
+    const double ior = s->mat_param[i];
+    r.inv_param = (float)(1.0 / ior);
+    const double r0 = (1.0 - ior) / (1.0 + ior);
+    r.r0 = (float)(r0 * r0);
   }
   bvh_builder bb;
   bb.run(s);
@@ -973,8 +978,8 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
   kp.oref2 = c->oref2;
   kp.seed32 = (uint32_t)prm->seed ^ ((uint32_t)(prm->seed >> 32) * 0x9E3779B9u);
   kp.flags = prm->flags;
-  kp.wm1 = (float)(prm->width - 1);
-  kp.hm1 = (float)(prm->height - 1);
+  kp.inv_wm1 = (float)(1.0 / (prm->width - 1));
+  kp.inv_hm1 = (float)(1.0 / (prm->height - 1));
   const int tiles_y = (prm->local_rows + rtk::kTile - 1) / rtk::kTile;
   const long long tiles = (long long)kp.tiles_x * tiles_y;
   const unsigned blocks = (unsigned)((tiles + rtk::kWavesPerBlock - 1) / rtk::kWavesPerBlock);
