@@ -20,7 +20,8 @@ from dataclasses import dataclass
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librtow.so")
+# RTOW_LIB: load an alternative build (A/B experiments on the GPU box)
+LIB_PATH = os.environ.get("RTOW_LIB") or os.path.join(HERE, "librtow.so")
 
 RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC = 0, 1, 2
 RT_CAMERA_CPU, RT_CAMERA_GPU = 0, 1
