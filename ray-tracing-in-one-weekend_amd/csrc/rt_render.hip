@@ -319,8 +319,11 @@ __device__ __forceinline__ float refine_root(const shade_rec &sr, float t_scan, 
   return t;
 }
 
+// 7 waves per SIMD: the register budget that admits it (<= 72 VGPRs, SGPRs
+// for 7 blocks/CU) measured 3.6 % faster than the unconstrained 6-wave build
+// and much faster than forcing 8 (scratch spills).
 template <bool OPEN, bool METAL_UNIT, bool BVH, bool STATS>
-__global__ __launch_bounds__(kBlock) void render_kernel(const kparams p,
+__global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
                                                         const pair_geom *__restrict__ scan_geom,
                                                         const pair_geom *__restrict__ geom,
                                                         const bvh_node *__restrict__ nodes,
