@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--accel", choices=["scan", "bvh"], default="bvh",
                     help="bvh: wave-uniform BVH walk (default; bit-identical result to the scan, "
                          "tested on the full headline frame); scan: brute-force closest hit")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl (= RCCL over xGMI); gloo only to rehearse the multi-process path "
+                         "on a one-GPU box (tiles staged through host memory)")
     ap.add_argument("--cpu-spp", type=int, default=30, help="spp of the bounded CPU sample (400x225)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--out", default="", help="write the gathered frame as PPM (P6 if .pgm/.p6)")
@@ -105,31 +108,41 @@ def main():
     import rtow
     import rtow_dist
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    n_dev = torch.cuda.device_count()
+    dev_idx = local_rank % n_dev  # == local_rank on a full node; wraps only for gloo rehearsal
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=dev)
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     W, H, spp = a.width, a.height, a.spp
     workload = f"final random-spheres scene {W}x{H} @ {spp}spp depth {a.depth}"
     scene = rtow.final_scene(a.half_extent)
     cam = rtow.camera_cpu(aspect=W / H)
-    ctx = rtow.Context(local_rank)
+    ctx = rtow.Context(dev_idx)
     ctx.upload(scene)
     params = rtow_dist.partition(W, H, spp, world, rank, a.row_block, max_depth=a.depth)
     params.flags |= rtow.RT_FLAG_KEEP_COUNTERS
     if a.accel == "bvh":
         params.flags |= rtow.RT_FLAG_ACCEL_BVH
     tile = torch.zeros((params.local_rows, W, 3), dtype=torch.float32, device=dev)
-    gather_list = [torch.empty_like(tile) for _ in range(world)] if (world > 1 and rank == 0) else None
+    gdev = dev if a.backend == "nccl" else torch.device("cpu")
+    gather_list = ([torch.empty(tile.shape, dtype=tile.dtype, device=gdev) for _ in range(world)]
+                   if (world > 1 and rank == 0) else None)
     # a dedicated stream: the kernel, the HIP events timing it and the RCCL gather
     # are all ordered on it (torch's default stream would reach the C ABI as NULL)
     stream = torch.cuda.Stream(dev)
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local_rank])
+            if a.backend == "nccl":
+                dist.barrier(device_ids=[dev_idx])
+            else:
+                dist.barrier()
 
     def step(i, events=None):
         params.seed = i
@@ -139,7 +152,7 @@ def main():
         if events is not None:
             events[1].record(stream)
         if world > 1:
-            dist.gather(tile, gather_list, dst=0)
+            dist.gather(tile if a.backend == "nccl" else tile.cpu(), gather_list, dst=0)
 
     assert stream.cuda_stream != 0
     with torch.cuda.stream(stream):
@@ -171,8 +184,8 @@ def main():
         torch.cuda.synchronize(dev)
     work = ctx.collect_stats()
     local = torch.tensor([float(st.segments), float(st.samples), float(st.wave_steps)],
-                         dtype=torch.float64, device=dev)
-    t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+                         dtype=torch.float64, device=gdev)
+    t_max = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
     if world > 1:
         dist.all_reduce(local, op=dist.ReduceOp.SUM)
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
