@@ -226,7 +226,8 @@ def main():
             "config": {"workload": workload, "width": W, "height": H, "spp": spp,
                        "max_depth": a.depth, "spheres": scene.n,
                        "parallelism": f"row-interleaved bands of {a.row_block} rows x {world} GPU"
-                                      + (" + RCCL gather" if world > 1 else "")},
+                                      + ((" + RCCL gather" if a.backend == "nccl" else " + gloo gather")
+                                         if world > 1 else "")},
             "ms_per_frame": round(elapsed / a.steps * 1e3, 3),
             "msamples_per_s": round(samples / elapsed / 1e6, 2),
             "segments_per_frame": int(segments / a.steps),
@@ -234,7 +235,7 @@ def main():
             "kernel_ms_avg_rank0": round(k_avg_s * 1e3, 3),
             "accel": a.accel,
             "work_per_launch_rank0": {"segments": work.segments, "sphere_tests": work.sphere_tests,
-                                      "box_tests": work.box_tests,
+                                      "box_tests": work.box_tests, "box_hits_own_ray": work.box_hits,
                                       "brute_force_equiv_tests": work.bf_tests},
             "roofline": {"bound": "valu", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),

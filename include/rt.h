@@ -133,6 +133,8 @@ typedef struct {
   uint64_t bf_tests;     /* brute-force equivalent ray-sphere tests: segments * spheres */
   uint64_t sphere_tests; /* executed lane-level ray-sphere tests (RT_FLAG_COUNT_WORK only) */
   uint64_t box_tests;    /* executed lane-level ray-box tests (RT_FLAG_COUNT_WORK only) */
+  uint64_t box_hits;     /* ... of which the lane's own ray entered the box (the rest are
+                            visits forced by other lanes of the wave) */
   uint64_t wave_steps;   /* sum over waves of bounce iterations (lane-efficiency denominator / 64) */
   double kernel_ms;      /* hipEvent time of the render kernel (0 if async) */
 } rt_stats;

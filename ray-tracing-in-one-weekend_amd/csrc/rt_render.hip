@@ -349,6 +349,7 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
   uint32_t sample = 0;
   uint32_t segs = 0, steps = 0;
   uint32_t lane_tests = 0, lane_boxes = 0;  // executed work, STATS builds only
+  uint32_t lane_box_hits = 0;               // boxes this lane's own ray entered
   bool alive = valid && p.spp > 0 && p.max_depth > 0;  // depth 0: black, no hit test
   if (alive) {
     camera_ray(p, pix, col, grow, 0u, ox, oy, oz, dx, dy, dz);
@@ -402,7 +403,10 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
           const f2 tz = fma2(nd.bz, viz, voz);
           const float tn = fmaxf(fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y)), 0.0f);
           const float tf = fminf(fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y)), hs.tmax);
-          if (STATS) ++lane_boxes;
+          if (STATS) {
+            ++lane_boxes;
+            lane_box_hits += (tn <= tf) ? 1u : 0u;
+          }
           if (__builtin_amdgcn_ballot_w64(tn <= tf)) {
             if (nd.leaf) {
               const int fp = (int)nd.leaf - 1;
@@ -534,13 +538,14 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
   }
   // one atomic per wave for the counters
   uint32_t s = segs;
-  uint64_t lt = lane_tests, lb = lane_boxes;
+  uint64_t lt = lane_tests, lb = lane_boxes, lh = lane_box_hits;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     s += __shfl_xor(s, off);
     if (STATS) {
       lt += __shfl_xor(lt, off);
       lb += __shfl_xor(lb, off);
+      lh += __shfl_xor(lh, off);
     }
   }
   if (lane == 0) {
@@ -549,6 +554,7 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
     if (STATS) {
       atomicAdd(&counters[2], (unsigned long long)lt);
       atomicAdd(&counters[3], (unsigned long long)lb);
+      atomicAdd(&counters[4], (unsigned long long)lh);
     }
   }
 }
@@ -863,7 +869,7 @@ int rt_context_create(int device_ordinal, rt_context **out) {
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) break;
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) break;
     if ((e = hipEventCreate(&c->ev1)) != hipSuccess) break;
-    if ((e = hipMalloc(&c->d_counters, 4 * sizeof(unsigned long long))) != hipSuccess) break;
+    if ((e = hipMalloc(&c->d_counters, 8 * sizeof(unsigned long long))) != hipSuccess) break;
   } while (0);
   if (e != hipSuccess) {
     st = hip_fail(e);
@@ -958,7 +964,7 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
   if (prm->flags & RT_FLAG_KEEP_COUNTERS) {
     c->last_samples += samples;
   } else {
-    RT_HIP(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long), st));
+    RT_HIP(hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), st));
     c->last_samples = samples;
   }
   c->last_stats = (prm->flags & RT_FLAG_COUNT_WORK) != 0;
@@ -998,7 +1004,7 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
 int rt_reset_stats(rt_context *c, void *stream) {
   if (!c) return RT_ERR_INVALID;
   RT_HIP(hipSetDevice(c->device));
-  RT_HIP(hipMemsetAsync(c->d_counters, 0, 4 * sizeof(unsigned long long),
+  RT_HIP(hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long),
                         stream ? (hipStream_t)stream : c->stream));
   c->last_samples = 0;
   return RT_OK;
@@ -1006,7 +1012,7 @@ int rt_reset_stats(rt_context *c, void *stream) {
 
 int rt_collect_stats(rt_context *c, rt_stats *stats) {
   if (!c || !stats) return RT_ERR_INVALID;
-  unsigned long long h[4] = {0, 0, 0, 0};
+  unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   RT_HIP(hipSetDevice(c->device));
   RT_HIP(hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
   stats->segments = h[0];
@@ -1015,6 +1021,7 @@ int rt_collect_stats(rt_context *c, rt_stats *stats) {
   stats->bf_tests = h[0] * (uint64_t)c->n_spheres;
   stats->sphere_tests = c->last_stats ? h[2] : 0;
   stats->box_tests = c->last_stats ? h[3] : 0;
+  stats->box_hits = c->last_stats ? h[4] : 0;
   stats->kernel_ms = 0.0;
   return RT_OK;
 }

@@ -66,7 +66,8 @@ class Params(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [("segments", ctypes.c_uint64), ("samples", ctypes.c_uint64),
                 ("bf_tests", ctypes.c_uint64), ("sphere_tests", ctypes.c_uint64),
-                ("box_tests", ctypes.c_uint64), ("wave_steps", ctypes.c_uint64),
+                ("box_tests", ctypes.c_uint64), ("box_hits", ctypes.c_uint64),
+                ("wave_steps", ctypes.c_uint64),
                 ("kernel_ms", ctypes.c_double)]
 
     def as_dict(self):
