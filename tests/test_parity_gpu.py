@@ -128,6 +128,20 @@ def test_bvh_equals_scan_headline_frame(rtow, gpu_ctx):
     assert n_diff == 0, n_diff
 
 
+def test_bvh_equals_scan_ten_thousand_spheres(rtow, gpu_ctx):
+    """BASELINE config 5's 10 000-sphere scene at 1920x1080 x 4 spp: the BVH walk
+    and the brute-force scan (10 004 tests per segment) agree on every sum."""
+    gpu_ctx.upload(rtow.final_scene(half_extent=50))
+    cam = rtow.camera_cpu(aspect=1920 / 1080)
+    p = rtow.make_params(1920, 1080, 4, seed=21, flags=1 << 10)
+    a, sa = gpu_ctx.render(cam, p)
+    p.flags |= 1 << 9
+    b, sb = gpu_ctx.render(cam, p)
+    assert sa.segments == sb.segments
+    assert np.array_equal(a, b)
+    assert sb.sphere_tests * 50 < sa.sphere_tests  # the BVH does >50x fewer sphere tests
+
+
 def test_empty_scene_all_sky(rtow, gpu_ctx, accel):
     s = rtow.final_scene()
     empty = rtow.Scene(s.cx[:0], s.cy[:0], s.cz[:0], s.radius[:0], s.kind[:0], s.albedo[:0], s.param[:0])
