@@ -137,6 +137,8 @@ typedef struct {
                             visits forced by other lanes of the wave) */
   uint64_t wave_steps;   /* sum over waves of bounce iterations (lane-efficiency denominator / 64) */
   double kernel_ms;      /* hipEvent time of the render kernel (0 if async) */
+  uint64_t root_tests;   /* RT_FLAG_COUNT_WORK: per alive lane and bounce, the spheres whose
+                            root / interval code the wave executed (some lane's line met it) */
 } rt_stats;
 
 typedef struct rt_context rt_context;

@@ -325,9 +325,13 @@ float cbrt01(float u) {
   return u == 0.0f ? 0.0f : c;
 }
 
+// sqrtf(max(x, 2^-96)): the kernel's sqrt_k (rt_render.hip) -- correctly
+// rounded, argument clamped below
+inline float sqrt_k(float x) { return std::sqrt(std::fmax(x, 0x1p-96f)); }
+
 void unit_vec(float u1, float u2, float &x, float &y, float &z) {
   z = fmaf_(-2.0f, u1, 1.0f);
-  float r = std::sqrt(std::fmax(fmaf_(-z, z, 1.0f), 0.0f));
+  float r = sqrt_k(fmaf_(-z, z, 1.0f));
   float s, c;
   sincos_turn(u2, s, c);
   x = r * c;
@@ -338,11 +342,19 @@ inline float dot3(float ax, float ay, float az, float bx, float by, float bz) {
   return fmaf_(az, bz, fmaf_(ay, by, ax * bx));
 }
 
+// the kernel's normalize3: integer-seeded inverse sqrt + 3 Newton steps
 void normalize3(float &x, float &y, float &z) {
-  float inv = 1.0f / std::sqrt(dot3(x, y, z, x, y, z));
-  x *= inv;
-  y *= inv;
-  z *= inv;
+  const float l2 = dot3(x, y, z, x, y, z);
+  uint32_t i;
+  std::memcpy(&i, &l2, 4);
+  i = 0x5f375a86u - (i >> 1);
+  float r;
+  std::memcpy(&r, &i, 4);
+  const float h = 0.5f * l2;
+  for (int k = 0; k < 3; ++k) r = r * fmaf_(-h, r * r, 1.5f);
+  x *= r;
+  y *= r;
+  z *= r;
 }
 
 struct kscene {
@@ -377,7 +389,7 @@ void camera_ray(const kctx &k, uint32_t pix, int col, int grow, uint32_t sample,
   for (int a = 0; a < 3; ++a) t[a] = fmaf_(ft, c.vert[a], fmaf_(fs, c.horiz[a], c.corner[a]));
   for (int a = 0; a < 3; ++a) o[a] = c.eye[a];
   if (c.has_lens) {
-    float rr = std::sqrt(unif(r.z));
+    float rr = sqrt_k(unif(r.z));
     float s, cc;
     sincos_turn(unif(r.w), s, cc);
     float ddx = rr * cc, ddy = rr * s;
@@ -421,7 +433,7 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
           // wins if closer than tmax (ties: last index for the closed src/cpu
           // interval, first for the open src/gpu one -- what a sequential scan
           // does, stated so that any visiting order gives the same winner)
-          const float sq = std::sqrt(e - sc.ks[i]);
+          const float sq = sqrt_k(e - sc.ks[i]);
           const float t0 = h - sq, t1 = h + sq;
           const bool use0 = k.open ? t0 > 0.001f : t0 >= 0.001f;
           const float root = use0 ? t0 : t1;
@@ -469,8 +481,7 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
         } else {
           disc = fmaf_(bb, bb, -cc);
         }
-        disc = std::fmax(disc, 0.0f);
-        const float sq = std::sqrt(disc);
+        const float sq = sqrt_k(disc);
         const float q = -(bb + (bb < 0.0f ? -sq : sq));
         if (q != 0.0f) {
           const float ta = q, tb = cc / q;
@@ -516,7 +527,7 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
       } else {
         const float ratio = front ? sc.inv_param[b] : sc.param[b];
         const float cos_t = std::fmin(-dot3(d[0], d[1], d[2], nn[0], nn[1], nn[2]), 1.0f);
-        const float sin_t = std::sqrt(fmaf_(-cos_t, cos_t, 1.0f));
+        const float sin_t = sqrt_k(fmaf_(-cos_t, cos_t, 1.0f));
         const bool cannot = ratio * sin_t > 1.0f;
         const float r0 = sc.r0[b];  // ((1-ior)/(1+ior))^2, same for ior and 1/ior
         const float x = 1.0f - cos_t;
@@ -528,7 +539,7 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
         } else {
           float q[3];
           for (int a = 0; a < 3; ++a) q[a] = ratio * fmaf_(cos_t, nn[a], d[a]);
-          const float m = -std::sqrt(std::fabs(1.0f - dot3(q[0], q[1], q[2], q[0], q[1], q[2])));
+          const float m = -sqrt_k(std::fabs(1.0f - dot3(q[0], q[1], q[2], q[0], q[1], q[2])));
           for (int a = 0; a < 3; ++a) sd[a] = fmaf_(m, nn[a], q[a]);
         }
       }

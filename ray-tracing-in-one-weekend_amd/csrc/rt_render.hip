@@ -101,6 +101,23 @@ __device__ __forceinline__ uint4 pcg4d(uint32_t a, uint32_t b, uint32_t c, uint3
 
 __device__ __forceinline__ float unif(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
 
+// sqrtf(max(x, 2^-96)), correctly rounded.  v_sqrt_f32 is within 1 ulp; the
+// two fma residuals pick the correctly rounded neighbour (LLVM's own expansion
+// of sqrtf).  Clamping the argument to >= 2^-96 removes the expansion's
+// denormal-range rescaling and its inf/nan fix-up: 10 VALU instead of 17.  No
+// call site can tell the clamp from sqrtf (arguments are 0 or >> 2^-96, and a
+// root 2^-48 instead of 0 rounds away against any t >= 0.001); the host
+// restatement applies the same clamp anyway.
+__device__ __forceinline__ float sqrt_k(float x) {
+  x = fmaxf(x, 0x1p-96f);
+  const float y = __builtin_amdgcn_sqrtf(x);
+  const float ydn = __uint_as_float(__float_as_uint(y) - 1u);
+  const float yup = __uint_as_float(__float_as_uint(y) + 1u);
+  float r = (fmaf(-ydn, y, x) <= 0.0f) ? ydn : y;
+  r = (fmaf(-yup, y, x) > 0.0f) ? yup : r;
+  return r;
+}
+
 // sin/cos of 2*pi*u, u in [0,1): quadrant from 4u (exact), Taylor on [0,pi/2).
 __device__ __forceinline__ void sincos_turn(float u, float &s, float &c) {
   float q4 = u * 4.0f;
@@ -143,19 +160,27 @@ __device__ __forceinline__ float cbrt01(float u) {
 // random_unit_vector, src/cpu/vec3.h:105-114; equal in distribution)
 __device__ __forceinline__ void unit_vec(float u1, float u2, float &x, float &y, float &z) {
   z = fmaf(-2.0f, u1, 1.0f);
-  float r = sqrtf(fmaxf(fmaf(-z, z, 1.0f), 0.0f));
+  float r = sqrt_k(fmaf(-z, z, 1.0f));
   float s, c;
   sincos_turn(u2, s, c);
   x = r * c;
   y = r * s;
 }
 
+// x * 1/|x| with 1/|x| from an integer-seeded inverse square root and three
+// Newton steps y <- y (3/2 - (l2/2) y^2): plain fp32 mul/fma, so the host
+// restatement reproduces it bit for bit, and ~12 VALU instead of a correctly
+// rounded sqrt followed by a correctly rounded division (~28).  |result| is 1
+// within a few ulp; l2 is never 0 or inf here ("Kernel").
 __device__ __forceinline__ void normalize3(float &x, float &y, float &z) {
-  float l2 = fmaf(z, z, fmaf(y, y, x * x));
-  float inv = 1.0f / sqrtf(l2);
-  x *= inv;
-  y *= inv;
-  z *= inv;
+  const float l2 = fmaf(z, z, fmaf(y, y, x * x));
+  float r = __uint_as_float(0x5f375a86u - (__float_as_uint(l2) >> 1));
+  const float h = 0.5f * l2;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) r = r * fmaf(-h, r * r, 1.5f);
+  x *= r;
+  y *= r;
+  z *= r;
 }
 
 __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {
@@ -185,7 +210,7 @@ __device__ __forceinline__ void camera_ray(const kparams &p, uint32_t pix, int c
   oy = p.cam.eye[1];
   oz = p.cam.eye[2];
   if (p.cam.has_lens) {
-    float rr = sqrtf(unif(r.z));
+    float rr = sqrt_k(unif(r.z));
     float s, c;
     sincos_turn(unif(r.w), s, c);
     float ddx = rr * c, ddy = rr * s;
@@ -221,7 +246,7 @@ struct hit_state {
 template <bool OPEN>
 __device__ __forceinline__ void candidate(bool c, float h, float disc, int idx, hit_state &hs) {
   if (c) {
-    const float sq = sqrtf(disc);
+    const float sq = sqrt_k(disc);
     const float t0 = h - sq, t1 = h + sq;
     const bool use0 = OPEN ? (t0 > 0.001f) : (t0 >= 0.001f);
     const float root = use0 ? t0 : t1;
@@ -245,10 +270,10 @@ struct ray_pre {
 // 7 v_pk_fma_f32 + 2 v_cmp; one scalar OR of the ballots decides whether any
 // lane needs the sqrt / interval work.  orig maps slots to original indices
 // (BVH order); nullptr = identity (brute-force order).
-template <bool OPEN, int NP>
+template <bool OPEN, int NP, bool STATS>
 __device__ __forceinline__ void scan_pairs(const pair_geom *__restrict__ g, int slot0,
                                            const int *__restrict__ orig, const ray_pre &r,
-                                           hit_state &hs) {
+                                           hit_state &hs, uint32_t &roots) {
   pair_geom q[NP];
   f2 h[NP], e[NP];
   bool c[2 * NP];
@@ -266,6 +291,10 @@ __device__ __forceinline__ void scan_pairs(const pair_geom *__restrict__ g, int 
 #pragma unroll
   for (int j = 0; j < 2 * NP; ++j) any |= __builtin_amdgcn_ballot_w64(c[j]);
   if (any) {  // wave-uniform: the rare path where some line meets a sphere
+    if (STATS) {
+#pragma unroll
+      for (int j = 0; j < 2 * NP; ++j) roots += __builtin_amdgcn_ballot_w64(c[j]) != 0 ? 1u : 0u;
+    }
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
       const int s0 = slot0 + 2 * j;
@@ -307,8 +336,7 @@ __device__ __forceinline__ float refine_root(const shade_rec &sr, float t_scan, 
   } else {
     disc = fmaf(b, b, -c);
   }
-  disc = fmaxf(disc, 0.0f);
-  const float sq = sqrtf(disc);
+  const float sq = sqrt_k(disc);  // clamps disc below at 2^-96 > 0
   const float q = -(b + (b < 0.0f ? -sq : sq));
   float t = t_scan;
   if (q != 0.0f) {
@@ -350,6 +378,7 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
   uint32_t segs = 0, steps = 0;
   uint32_t lane_tests = 0, lane_boxes = 0;  // executed work, STATS builds only
   uint32_t lane_box_hits = 0;               // boxes this lane's own ray entered
+  uint32_t lane_roots = 0;                  // root/interval sequences the wave ran
   bool alive = valid && p.spp > 0 && p.max_depth > 0;  // depth 0: black, no hit test
   if (alive) {
     camera_ray(p, pix, col, grow, 0u, ox, oy, oz, dx, dy, dz);
@@ -373,7 +402,7 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
       const bool scan_all = !BVH || __builtin_amdgcn_ballot_w64(o2 > p.oref2) != 0;
       if (scan_all) {
         // brute force: 8 spheres (4 pairs) per iteration over the whole array
-        for (int k = 0; k < n_pairs; k += 4) scan_pairs<OPEN, 4>(scan_geom + k, 2 * k, nullptr, rp, hs);
+        for (int k = 0; k < n_pairs; k += 4) scan_pairs<OPEN, 4, STATS>(scan_geom + k, 2 * k, nullptr, rp, hs, lane_roots);
         if (STATS) lane_tests += 2 * n_pairs;
       } else {
         // wave-uniform stackless BVH walk: a node is entered if ANY lane's ray
@@ -410,7 +439,7 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
           if (__builtin_amdgcn_ballot_w64(tn <= tf)) {
             if (nd.leaf) {
               const int fp = (int)nd.leaf - 1;
-              scan_pairs<OPEN, kLeafPairs>(geom + fp, 2 * fp, orig, rp, hs);
+              scan_pairs<OPEN, kLeafPairs, STATS>(geom + fp, 2 * fp, orig, rp, hs, lane_roots);
               if (STATS) lane_tests += 2 * kLeafPairs;
               node = nd.skip;
             } else {
@@ -481,7 +510,7 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
           // dielectric, material.h:57-87 (r0 is the same for ior and 1/ior)
           const float ratio = front ? sr.inv_param : sr.param;
           const float cos_t = fminf(-dn, 1.0f);
-          const float sin_t = sqrtf(fmaf(-cos_t, cos_t, 1.0f));
+          const float sin_t = sqrt_k(fmaf(-cos_t, cos_t, 1.0f));
           const bool cannot = ratio * sin_t > 1.0f;
           const float x = 1.0f - cos_t;
           const float x2 = x * x;
@@ -494,7 +523,7 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
             const float qx = ratio * fmaf(cos_t, nx, dx);
             const float qy = ratio * fmaf(cos_t, ny, dy);
             const float qz = ratio * fmaf(cos_t, nz, dz);
-            const float m = -sqrtf(fabsf(1.0f - dot3(qx, qy, qz, qx, qy, qz)));
+            const float m = -sqrt_k(fabsf(1.0f - dot3(qx, qy, qz, qx, qy, qz)));
             sx = fmaf(m, nx, qx);
             sy = fmaf(m, ny, qy);
             sz = fmaf(m, nz, qz);
@@ -538,7 +567,7 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
   }
   // one atomic per wave for the counters
   uint32_t s = segs;
-  uint64_t lt = lane_tests, lb = lane_boxes, lh = lane_box_hits;
+  uint64_t lt = lane_tests, lb = lane_boxes, lh = lane_box_hits, lr = lane_roots;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     s += __shfl_xor(s, off);
@@ -546,6 +575,7 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
       lt += __shfl_xor(lt, off);
       lb += __shfl_xor(lb, off);
       lh += __shfl_xor(lh, off);
+      lr += __shfl_xor(lr, off);
     }
   }
   if (lane == 0) {
@@ -555,6 +585,7 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
       atomicAdd(&counters[2], (unsigned long long)lt);
       atomicAdd(&counters[3], (unsigned long long)lb);
       atomicAdd(&counters[4], (unsigned long long)lh);
+      atomicAdd(&counters[5], (unsigned long long)lr);
     }
   }
 }
@@ -1022,6 +1053,7 @@ int rt_collect_stats(rt_context *c, rt_stats *stats) {
   stats->sphere_tests = c->last_stats ? h[2] : 0;
   stats->box_tests = c->last_stats ? h[3] : 0;
   stats->box_hits = c->last_stats ? h[4] : 0;
+  stats->root_tests = c->last_stats ? h[5] : 0;
   stats->kernel_ms = 0.0;
   return RT_OK;
 }

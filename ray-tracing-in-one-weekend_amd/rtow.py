@@ -68,7 +68,7 @@ class Stats(ctypes.Structure):
                 ("bf_tests", ctypes.c_uint64), ("sphere_tests", ctypes.c_uint64),
                 ("box_tests", ctypes.c_uint64), ("box_hits", ctypes.c_uint64),
                 ("wave_steps", ctypes.c_uint64),
-                ("kernel_ms", ctypes.c_double)]
+                ("kernel_ms", ctypes.c_double), ("root_tests", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
