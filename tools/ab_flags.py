@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""A/B kernel time of render flags on one frame (default: headline 3840x2160x500).
+
+    python tools/ab_flags.py [--w --h --spp] [--reps 2] FLAGS_A FLAGS_B ...
+
+Each FLAGS_* is a '+'-joined list of rtow flag names without the RT_FLAG_
+prefix (e.g. ACCEL_BVH+SPLIT_PRIMARY) or 0.  Prints kernel ms per variant and
+checks that all variants produce identical sums.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ray-tracing-in-one-weekend_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--w", type=int, default=3840)
+    ap.add_argument("--h", type=int, default=2160)
+    ap.add_argument("--spp", type=int, default=500)
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--half-extent", type=int, default=11)
+    ap.add_argument("variants", nargs="+")
+    a = ap.parse_args()
+    import rtow
+    ctx = rtow.Context(0)
+    ctx.upload(rtow.final_scene(half_extent=a.half_extent))
+    cam = rtow.camera_cpu(aspect=a.w / a.h)
+    ref = None
+    for v in a.variants:
+        flags = 0
+        for name in v.split("+"):
+            if name != "0":
+                flags |= getattr(rtow, "RT_FLAG_" + name)
+        ms = []
+        for _ in range(a.reps):
+            img, st = ctx.render(cam, rtow.make_params(a.w, a.h, a.spp, seed=0, flags=flags))
+            ms.append(st.kernel_ms)
+        same = None
+        if ref is None:
+            ref = img
+        else:
+            same = bool(np.array_equal(ref, img))
+        print(json.dumps({"variant": v, "kernel_ms": [round(x, 3) for x in ms], "segments": st.segments,
+                          "identical_to_first": same}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

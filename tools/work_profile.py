@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--accel", default="bvh", choices=["bvh", "scan"])
     ap.add_argument("--half-extent", type=int, default=11)
+    ap.add_argument("--depth", type=int, default=50)
     a = ap.parse_args()
     import rtow
     ctx = rtow.Context(0)
@@ -30,10 +31,10 @@ def main():
     ctx.upload(scene)
     cam = rtow.camera_cpu(aspect=a.w / a.h)
     flags = rtow.RT_FLAG_COUNT_WORK | (rtow.RT_FLAG_ACCEL_BVH if a.accel == "bvh" else 0)
-    _, st = ctx.render(cam, rtow.make_params(a.w, a.h, a.spp, seed=0, flags=flags))
+    _, st = ctx.render(cam, rtow.make_params(a.w, a.h, a.spp, max_depth=a.depth, seed=0, flags=flags))
     seg = st.segments
     out = {
-        "workload": f"{a.w}x{a.h}x{a.spp} spheres={scene.n} accel={a.accel}",
+        "workload": f"{a.w}x{a.h}x{a.spp} depth={a.depth} spheres={scene.n} accel={a.accel}",
         "segments": seg,
         "lane_efficiency": round(seg / (64.0 * st.wave_steps), 4),
         "box_visits_per_seg": round(st.box_tests / seg, 3),
