@@ -233,8 +233,10 @@ __device__ __forceinline__ bool in_range(float t, float tmin, float tmax) {
 // running closest hit of one lane (hittable_list::hit's closest_so_far/rec)
 struct hit_state {
   float tmax;
-  int best;   // original sphere index, -1 = miss
-  bool near;  // the winner was taken at its entering root
+  int best;  // original sphere index, -1 = miss
+  int near;  // 1: the winner was taken at its entering root (an int, not a
+             // bool: a loop-carried bool becomes an SGPR lane mask merged with
+             // exec on every node of the walk)
 };
 
 // closest-hit candidate update (sphere.h:34-44 with a = |d|^2 = 1).  The root
@@ -256,7 +258,7 @@ __device__ __forceinline__ void candidate(bool c, float h, float disc, int idx, 
     if (above & closer) {
       hs.tmax = root;
       hs.best = idx;
-      hs.near = use0;
+      hs.near = use0 ? 1 : 0;
     }
   }
 }
@@ -347,6 +349,86 @@ __device__ __forceinline__ float refine_root(const shade_rec &sr, float t_scan, 
   return t;
 }
 
+// executed-work counters of one lane (RT_FLAG_COUNT_WORK builds only)
+struct work_ctr {
+  uint32_t tests = 0;     // ray-sphere tests
+  uint32_t boxes = 0;     // ray-box tests
+  uint32_t box_hits = 0;  // ... boxes this lane's own ray entered
+  uint32_t roots = 0;     // root/interval sequences the wave ran
+};
+
+// Closest hit of the ray (o, d) over all spheres: hittable_list::hit,
+// src/cpu/hittable_list.h:28-43.  Wave-uniform: every active lane of the wave
+// calls it together; the result does not depend on which lanes those are.
+template <bool OPEN, bool BVH, bool STATS>
+__device__ __forceinline__ hit_state closest_hit(const kparams &p, const pair_geom *__restrict__ scan_geom,
+                                                 const pair_geom *__restrict__ geom,
+                                                 const bvh_node *__restrict__ nodes,
+                                                 const int *__restrict__ orig, float ox, float oy, float oz,
+                                                 float dx, float dy, float dz, work_ctr &wc) {
+  const int n_pairs = p.n_pad / 2;
+  const float nk1 = -dot3(ox, oy, oz, dx, dy, dz);
+  const float o2 = dot3(ox, oy, oz, ox, oy, oz);
+  const float ox2 = -2.0f * ox, oy2 = -2.0f * oy, oz2 = -2.0f * oz;
+  hit_state hs{__builtin_huge_valf(), -1, 1};
+  const ray_pre rp{{dx, dx}, {dy, dy}, {dz, dz}, {nk1, nk1},
+                   {o2, o2}, {ox2, ox2}, {oy2, oy2}, {oz2, oz2}};
+  // the BVH boxes are padded for ray origins within |O| <= oref (see
+  // bvh_builder); a wave-step with any lane beyond that scans everything
+  const bool scan_all = !BVH || __builtin_amdgcn_ballot_w64(o2 > p.oref2) != 0;
+  if (scan_all) {
+    // brute force: 8 spheres (4 pairs) per iteration over the whole array
+    for (int k = 0; k < n_pairs; k += 4) scan_pairs<OPEN, 4, STATS>(scan_geom + k, 2 * k, nullptr, rp, hs, wc.roots);
+    if (STATS) wc.tests += 2 * n_pairs;
+  } else {
+    // wave-uniform stackless BVH walk: a node is entered if ANY lane's ray
+    // meets its (conservatively padded) box before that lane's tmax
+    // |d| components are clamped away from 0 before the reciprocal: an
+    // exactly axis-parallel ray (it happens ~20 times per 4K frame) would
+    // otherwise give slab bounds (-inf, inf - inf = NaN), and IEEE min/max
+    // then return -inf, culling a box the ray is inside.  With the clamp
+    // every slab value is finite; the ray bends by < 1e-14 over any length.
+    const float ix = __builtin_amdgcn_rcpf(fabsf(dx) < 1e-18f ? copysignf(1e-18f, dx) : dx);
+    const float iy = __builtin_amdgcn_rcpf(fabsf(dy) < 1e-18f ? copysignf(1e-18f, dy) : dy);
+    const float iz = __builtin_amdgcn_rcpf(fabsf(dz) < 1e-18f ? copysignf(1e-18f, dz) : dz);
+    const f2 vix = {ix, ix}, viy = {iy, iy}, viz = {iz, iz};
+    const f2 vox = {-ox * ix, -ox * ix}, voy = {-oy * iy, -oy * iy}, voz = {-oz * iz, -oz * iz};
+    // the wave walks the DFS order of its majority direction octant, so
+    // coherent rays visit near children first and tmax culls the rest
+    const uint32_t half = __builtin_popcountll(__builtin_amdgcn_ballot_w64(true)) / 2;
+    const int oct = (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dx < 0.0f)) > half ? 1 : 0) |
+                    (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dy < 0.0f)) > half ? 2 : 0) |
+                    (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dz < 0.0f)) > half ? 4 : 0);
+    const bvh_node *__restrict__ order = nodes + (size_t)oct * p.n_nodes;
+    int node = 0;
+    while (node < p.n_nodes) {
+      const bvh_node nd = order[node];
+      const f2 tx = fma2(nd.bx, vix, vox);
+      const f2 ty = fma2(nd.by, viy, voy);
+      const f2 tz = fma2(nd.bz, viz, voz);
+      const float tn = fmaxf(fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y)), 0.0f);
+      const float tf = fminf(fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y)), hs.tmax);
+      if (STATS) {
+        ++wc.boxes;
+        wc.box_hits += (tn <= tf) ? 1u : 0u;
+      }
+      if (__builtin_amdgcn_ballot_w64(tn <= tf)) {
+        if (nd.leaf) {
+          const int fp = (int)nd.leaf - 1;
+          scan_pairs<OPEN, kLeafPairs, STATS>(geom + fp, 2 * fp, orig, rp, hs, wc.roots);
+          if (STATS) wc.tests += 2 * kLeafPairs;
+          node = nd.skip;
+        } else {
+          node = node + 1;
+        }
+      } else {
+        node = nd.skip;
+      }
+    }
+  }
+  return hs;
+}
+
 // 7 waves per SIMD: the register budget that admits it (<= 72 VGPRs, SGPRs
 // for 7 blocks/CU) measured 3.6 % faster than the unconstrained 6-wave build
 // and much faster than forcing 8 (scratch spills).
@@ -376,80 +458,22 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
   int depth = 0;
   uint32_t sample = 0;
   uint32_t segs = 0, steps = 0;
-  uint32_t lane_tests = 0, lane_boxes = 0;  // executed work, STATS builds only
-  uint32_t lane_box_hits = 0;               // boxes this lane's own ray entered
-  uint32_t lane_roots = 0;                  // root/interval sequences the wave ran
+  work_ctr wc;  // executed work, STATS builds only
   bool alive = valid && p.spp > 0 && p.max_depth > 0;  // depth 0: black, no hit test
   if (alive) {
     camera_ray(p, pix, col, grow, 0u, ox, oy, oz, dx, dy, dz);
     sample = 1;
   }
 
-  const int n_pairs = p.n_pad / 2;
-  while (__ballot(alive)) {
+  while (true) {
+    hit_state hs{__builtin_huge_valf(), -1, 1};
+    if (!__ballot(alive)) break;
+    if (alive) hs = closest_hit<OPEN, BVH, STATS>(p, scan_geom, geom, nodes, orig, ox, oy, oz, dx, dy, dz, wc);
     ++steps;
     if (alive) {
       ++segs;
-      // ---- closest hit over all spheres (hittable_list::hit) ----
-      const float nk1 = -dot3(ox, oy, oz, dx, dy, dz);
       const float o2 = dot3(ox, oy, oz, ox, oy, oz);
       const float ox2 = -2.0f * ox, oy2 = -2.0f * oy, oz2 = -2.0f * oz;
-      hit_state hs{__builtin_huge_valf(), -1, true};
-      const ray_pre rp{{dx, dx}, {dy, dy}, {dz, dz}, {nk1, nk1},
-                       {o2, o2}, {ox2, ox2}, {oy2, oy2}, {oz2, oz2}};
-      // the BVH boxes are padded for ray origins within |O| <= oref (see
-      // bvh_builder); a wave-step with any lane beyond that scans everything
-      const bool scan_all = !BVH || __builtin_amdgcn_ballot_w64(o2 > p.oref2) != 0;
-      if (scan_all) {
-        // brute force: 8 spheres (4 pairs) per iteration over the whole array
-        for (int k = 0; k < n_pairs; k += 4) scan_pairs<OPEN, 4, STATS>(scan_geom + k, 2 * k, nullptr, rp, hs, lane_roots);
-        if (STATS) lane_tests += 2 * n_pairs;
-      } else {
-        // wave-uniform stackless BVH walk: a node is entered if ANY lane's ray
-        // meets its (conservatively padded) box before that lane's tmax
-        // |d| components are clamped away from 0 before the reciprocal: an
-        // exactly axis-parallel ray (it happens ~20 times per 4K frame) would
-        // otherwise give slab bounds (-inf, inf - inf = NaN), and IEEE min/max
-        // then return -inf, culling a box the ray is inside.  With the clamp
-        // every slab value is finite; the ray bends by < 1e-14 over any length.
-        const float ix = __builtin_amdgcn_rcpf(fabsf(dx) < 1e-18f ? copysignf(1e-18f, dx) : dx);
-        const float iy = __builtin_amdgcn_rcpf(fabsf(dy) < 1e-18f ? copysignf(1e-18f, dy) : dy);
-        const float iz = __builtin_amdgcn_rcpf(fabsf(dz) < 1e-18f ? copysignf(1e-18f, dz) : dz);
-        const f2 vix = {ix, ix}, viy = {iy, iy}, viz = {iz, iz};
-        const f2 vox = {-ox * ix, -ox * ix}, voy = {-oy * iy, -oy * iy}, voz = {-oz * iz, -oz * iz};
-        // the wave walks the DFS order of its majority direction octant, so
-        // coherent rays visit near children first and tmax culls the rest
-        const uint32_t half = __builtin_popcountll(__builtin_amdgcn_ballot_w64(true)) / 2;
-        const int oct = (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dx < 0.0f)) > half ? 1 : 0) |
-                        (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dy < 0.0f)) > half ? 2 : 0) |
-                        (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dz < 0.0f)) > half ? 4 : 0);
-        const bvh_node *__restrict__ order = nodes + (size_t)oct * p.n_nodes;
-        int node = 0;
-        while (node < p.n_nodes) {
-          const bvh_node nd = order[node];
-          const f2 tx = fma2(nd.bx, vix, vox);
-          const f2 ty = fma2(nd.by, viy, voy);
-          const f2 tz = fma2(nd.bz, viz, voz);
-          const float tn = fmaxf(fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y)), 0.0f);
-          const float tf = fminf(fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y)), hs.tmax);
-          if (STATS) {
-            ++lane_boxes;
-            lane_box_hits += (tn <= tf) ? 1u : 0u;
-          }
-          if (__builtin_amdgcn_ballot_w64(tn <= tf)) {
-            if (nd.leaf) {
-              const int fp = (int)nd.leaf - 1;
-              scan_pairs<OPEN, kLeafPairs, STATS>(geom + fp, 2 * fp, orig, rp, hs, lane_roots);
-              if (STATS) lane_tests += 2 * kLeafPairs;
-              node = nd.skip;
-            } else {
-              node = node + 1;
-            }
-          } else {
-            node = nd.skip;
-          }
-        }
-      }
       const float tmax = hs.tmax;
       const int best = hs.best;
       const bool near = hs.near;
@@ -548,7 +572,13 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
       }
       if (path_done) {
         if (sample < (uint32_t)p.spp) {
-          camera_ray(p, pix, col, grow, sample, ox, oy, oz, dx, dy, dz);
+          // camera constants are re-read from the kernel-argument segment
+          // here (scalar loads, cache hits) instead of being held in SGPRs
+          // for the whole kernel: the empty asm hides the pointer's
+          // invariance so the loads stay at this (only) use
+          const kparams *pk = (const kparams *)__builtin_amdgcn_kernarg_segment_ptr();
+          asm volatile("" : "+s"(pk));
+          camera_ray(*pk, pix, col, grow, sample, ox, oy, oz, dx, dy, dz);
           ++sample;
           depth = 0;
           thr = thg = thb = 1.0f;
@@ -567,7 +597,7 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
   }
   // one atomic per wave for the counters
   uint32_t s = segs;
-  uint64_t lt = lane_tests, lb = lane_boxes, lh = lane_box_hits, lr = lane_roots;
+  uint64_t lt = wc.tests, lb = wc.boxes, lh = wc.box_hits, lr = wc.roots;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     s += __shfl_xor(s, off);

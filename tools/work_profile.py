@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--accel", default="bvh", choices=["bvh", "scan"])
     ap.add_argument("--half-extent", type=int, default=11)
     ap.add_argument("--depth", type=int, default=50)
+    ap.add_argument("--flags", default="", help="extra '+'-joined RT_FLAG_ names, e.g. SORT_RAYS")
     a = ap.parse_args()
     import rtow
     ctx = rtow.Context(0)
@@ -31,10 +32,12 @@ def main():
     ctx.upload(scene)
     cam = rtow.camera_cpu(aspect=a.w / a.h)
     flags = rtow.RT_FLAG_COUNT_WORK | (rtow.RT_FLAG_ACCEL_BVH if a.accel == "bvh" else 0)
+    for name in filter(None, a.flags.split("+")):
+        flags |= getattr(rtow, "RT_FLAG_" + name)
     _, st = ctx.render(cam, rtow.make_params(a.w, a.h, a.spp, max_depth=a.depth, seed=0, flags=flags))
     seg = st.segments
     out = {
-        "workload": f"{a.w}x{a.h}x{a.spp} depth={a.depth} spheres={scene.n} accel={a.accel}",
+        "workload": f"{a.w}x{a.h}x{a.spp} depth={a.depth} spheres={scene.n} accel={a.accel} {a.flags}",
         "segments": seg,
         "lane_efficiency": round(seg / (64.0 * st.wave_steps), 4),
         "box_visits_per_seg": round(st.box_tests / seg, 3),
