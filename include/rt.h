@@ -124,8 +124,17 @@ typedef struct {
   int32_t band_offset;
   int32_t local_rows;
   uint32_t flags;
-  uint32_t reserved;
+  /* scheduling, not semantics: split every pixel's sample chunks (see
+   * RT_CHUNK_SPP) over this many waves; 0 = choose from the tile count (1 for
+   * a 4K frame on one GPU, more when a rank's share of the frame is small) */
+  uint32_t units;
 } rt_params;
+
+/* Summation order of a pixel (part of the result, like the RNG): samples are
+ * accumulated in order within chunks of RT_CHUNK_SPP samples, and the chunk
+ * sums are added in chunk order.  Chunks can then be traced by different
+ * waves (rt_params.units) without changing a single bit of the image. */
+#define RT_CHUNK_SPP 64
 
 typedef struct {
   uint64_t segments;     /* closest-hit queries (= hittable_list::hit calls) */

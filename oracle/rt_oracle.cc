@@ -405,7 +405,12 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
   const uint32_t pix = (uint32_t)grow * (uint32_t)k.p->width + (uint32_t)col;
   const size_t n = sc.cx.size();
   unsigned long long segs = 0;
+  // two-level sum (the kernel's spec, include/rt.h RT_CHUNK_SPP): samples
+  // accumulate in order within chunks of RT_CHUNK_SPP, the chunk sums are
+  // added in chunk order -- so a pixel's chunks may be traced by different
+  // waves and the result does not depend on how they are split
   acc[0] = acc[1] = acc[2] = 0.0f;
+  float c[3] = {0.0f, 0.0f, 0.0f};
   if (k.p->max_depth <= 0) return 0;  // ray_color(.., 0) is black, no hit test
   for (uint32_t sample = 0; sample < (uint32_t)k.p->spp; ++sample) {
     float o[3], d[3];
@@ -453,9 +458,9 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
       if (best < 0) {  // sky, main.cc:27-29
         const float a = 0.5f * (d[1] + 1.0f);
         const float s0 = 1.0f - a;
-        acc[0] = fmaf_(th[0], fmaf_(a, 0.5f, s0), acc[0]);
-        acc[1] = fmaf_(th[1], fmaf_(a, 0.7f, s0), acc[1]);
-        acc[2] = fmaf_(th[2], s0 + a, acc[2]);
+        c[0] = fmaf_(th[0], fmaf_(a, 0.5f, s0), c[0]);
+        c[1] = fmaf_(th[1], fmaf_(a, 0.7f, s0), c[1]);
+        c[2] = fmaf_(th[2], s0 + a, c[2]);
         break;
       }
       const size_t b = (size_t)best;
@@ -550,6 +555,12 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
         d[a] = sd[a];
       }
       normalize3(d[0], d[1], d[2]);
+    }
+    if ((sample + 1) % RT_CHUNK_SPP == 0 || sample + 1 == (uint32_t)k.p->spp) {
+      for (int a = 0; a < 3; ++a) {
+        acc[a] += c[a];
+        c[a] = 0.0f;
+      }
     }
   }
   return segs;

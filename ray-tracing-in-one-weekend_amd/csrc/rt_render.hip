@@ -42,6 +42,12 @@ constexpr int kTile = 8;           // 8x8 pixels per wave
 constexpr int kWavesPerBlock = 4;  // 256 threads
 constexpr int kBlock = 64 * kWavesPerBlock;
 constexpr int kSpherePad = 8;      // scan unroll granularity
+// auto rt_params.units: below kSplitTiles tiles (12 waves per wave slot of
+// the chip: 256 CUs x 4 SIMDs x 7) every chunk gets its own wave; above it a
+// wave traces all of its tile's samples.  Measured on the headline frame
+// (tools/rank_times.py): 1 GPU (129 600 tiles) 466 ms unsplit vs
+// 483 split; a 1/8 share (16 320 tiles) 151 ms unsplit vs 65 split.
+constexpr long long kSplitTiles = 12LL * 256 * 4 * 7;
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -83,6 +89,10 @@ struct kparams {
   float oref2;  // BVH padding assumes |ray origin|^2 <= oref2 (else the wave scans)
   uint32_t seed32, flags;
   float inv_wm1, inv_hm1;  // 1/(W-1), 1/(H-1) rounded once (cpu camera model)
+  // sample chunks (RT_CHUNK_SPP) and their split over waves: block b traces
+  // chunks [u*cpu, (u+1)*cpu) of its tiles, u = b % units, cpu = chunks_per_unit
+  int n_chunks, units, chunks_per_unit, pad_;
+  uint64_t chunk_stride;  // floats per chunk plane (local_rows * width * 3)
 };
 
 // ---------------------------------------------------------------- RNG ----
@@ -440,9 +450,11 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
                                                         const int *__restrict__ orig,
                                                         const shade_rec *__restrict__ shade,
                                                         float *__restrict__ out,
+                                                        float *__restrict__ chunks,
                                                         unsigned long long *__restrict__ counters) {
   const int lane = threadIdx.x & 63;
-  const int tile = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  const int unit = (int)(blockIdx.x % (unsigned)p.units);
+  const int tile = (int)(blockIdx.x / (unsigned)p.units) * kWavesPerBlock + (threadIdx.x >> 6);
   const int tx = tile % p.tiles_x, ty = tile / p.tiles_x;
   const int col = tx * kTile + (lane & (kTile - 1));
   const int lrow = ty * kTile + (lane >> 3);
@@ -459,10 +471,18 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
   uint32_t sample = 0;
   uint32_t segs = 0, steps = 0;
   work_ctr wc;  // executed work, STATS builds only
-  bool alive = valid && p.spp > 0 && p.max_depth > 0;  // depth 0: black, no hit test
+  // this wave's samples: chunks [unit*cpu, (unit+1)*cpu) of RT_CHUNK_SPP each
+  const uint32_t s_begin = (uint32_t)(unit * p.chunks_per_unit) * RT_CHUNK_SPP;
+  const uint32_t s_end = min((uint32_t)((unit + 1) * p.chunks_per_unit) * RT_CHUNK_SPP, (uint32_t)p.spp);
+  // two-level sum: acc* hold the current chunk's sum; unit 0 folds finished
+  // chunks into s_tot (LDS, no registers), later units store theirs for
+  // fold_chunks
+  __shared__ float s_tot[3][kBlock];
+  s_tot[0][threadIdx.x] = s_tot[1][threadIdx.x] = s_tot[2][threadIdx.x] = 0.0f;
+  bool alive = valid && s_end > s_begin && p.max_depth > 0;  // depth 0: black, no hit test
   if (alive) {
-    camera_ray(p, pix, col, grow, 0u, ox, oy, oz, dx, dy, dz);
-    sample = 1;
+    camera_ray(p, pix, col, grow, s_begin, ox, oy, oz, dx, dy, dz);
+    sample = s_begin + 1;
   }
 
   while (true) {
@@ -571,7 +591,21 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
         }
       }
       if (path_done) {
-        if (sample < (uint32_t)p.spp) {
+        if (sample % RT_CHUNK_SPP == 0 || sample == s_end) {  // the path closed a chunk
+          if (unit == 0) {
+            s_tot[0][threadIdx.x] += accr;
+            s_tot[1][threadIdx.x] += accg;
+            s_tot[2][threadIdx.x] += accb;
+          } else {
+            float *c = chunks + (size_t)((sample - 1) / RT_CHUNK_SPP) * p.chunk_stride +
+                       3 * ((size_t)lrow * p.width + col);
+            c[0] = accr;
+            c[1] = accg;
+            c[2] = accb;
+          }
+          accr = accg = accb = 0.0f;
+        }
+        if (sample < s_end) {
           // camera constants are re-read from the kernel-argument segment
           // here (scalar loads, cache hits) instead of being held in SGPRs
           // for the whole kernel: the empty asm hides the pointer's
@@ -589,11 +623,11 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
     }
   }
 
-  if (in_tile) {
+  if (in_tile && unit == 0) {  // padding pixels (row >= height) write zeros
     float *o = out + 3 * ((size_t)lrow * p.width + col);
-    o[0] = accr;
-    o[1] = accg;
-    o[2] = accb;
+    o[0] = s_tot[0][threadIdx.x];
+    o[1] = s_tot[1][threadIdx.x];
+    o[2] = s_tot[2][threadIdx.x];
   }
   // one atomic per wave for the counters
   uint32_t s = segs;
@@ -620,6 +654,24 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
   }
 }
 
+// out += chunk sums of the waves with unit > 0, in chunk order (the left fold
+// of RT_CHUNK_SPP's two-level sum; unit 0 already folded chunks [0, first)).
+// Memory-bound and tiny: (n_chunks - first) planes read once.
+__global__ __launch_bounds__(256) void fold_chunks(const float *__restrict__ chunks, float *__restrict__ out,
+                                                   int first, int n_chunks, uint64_t stride, int width,
+                                                   int height, int row_block, int band_stride,
+                                                   int band_offset) {
+  for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < stride; j += (uint64_t)gridDim.x * 256u) {
+    const int lrow = (int)(j / (3u * (uint64_t)width));
+    const int band = lrow / row_block;
+    const int grow = (band * band_stride + band_offset) * row_block + (lrow - band * row_block);
+    if (grow >= height) continue;  // padding rows stay zero
+    float acc = out[j];
+    for (int k = first; k < n_chunks; ++k) acc += chunks[(uint64_t)k * stride + j];
+    out[j] = acc;
+  }
+}
+
 }  // namespace rtk
 
 // ------------------------------------------------------------ context ----
@@ -637,6 +689,8 @@ struct rt_context {
   unsigned long long *d_counters = nullptr;
   float *d_frame = nullptr;
   size_t frame_floats = 0;
+  float *d_chunks = nullptr;  // chunk sums of units > 0 (RT_CHUNK_SPP), grown on demand
+  size_t chunk_floats = 0;
   uint64_t last_samples = 0;
   bool last_stats = false;
 };
@@ -858,12 +912,12 @@ void fill_slot(rtk::pair_geom &g, int l, const rt_scene_view *s, int i) {
 }
 
 template <bool O, bool U, bool B, bool S>
-void launch(unsigned blocks, hipStream_t st, const rtk::kparams &kp, rt_context *c, float *out) {
+void launch(unsigned blocks, hipStream_t st, const rtk::kparams &kp, rt_context *c, float *out, float *chunks) {
   rtk::render_kernel<O, U, B, S><<<blocks, rtk::kBlock, 0, st>>>(
-      kp, c->d_geom, c->d_bvh_geom, c->d_nodes, c->d_orig, c->d_shade, out, c->d_counters);
+      kp, c->d_geom, c->d_bvh_geom, c->d_nodes, c->d_orig, c->d_shade, out, chunks, c->d_counters);
 }
 
-using launch_fn = void (*)(unsigned, hipStream_t, const rtk::kparams &, rt_context *, float *);
+using launch_fn = void (*)(unsigned, hipStream_t, const rtk::kparams &, rt_context *, float *, float *);
 // index: open | unit<<1 | bvh<<2 | stats<<3
 const launch_fn kLaunch[16] = {
     launch<false, false, false, false>, launch<true, false, false, false>,
@@ -948,6 +1002,7 @@ void rt_context_destroy(rt_context *c) {
   free_scene(c);
   (void)hipFree(c->d_counters);
   (void)hipFree(c->d_frame);
+  (void)hipFree(c->d_chunks);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1057,8 +1112,44 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
                 ((prm->flags & RT_FLAG_METAL_UNIT_VECTOR) ? 2 : 0) |
                 ((prm->flags & RT_FLAG_ACCEL_BVH) ? 4 : 0) |
                 ((prm->flags & RT_FLAG_COUNT_WORK) ? 8 : 0);
-  kLaunch[v](blocks, st, kp, c, accum_rgb);
+  // sample chunks (RT_CHUNK_SPP) and how many waves share a tile's chunks.
+  // One wave per tile traces all of a pixel's samples in sequence; when a
+  // rank holds few tiles (a 1/8 share of a 4K frame is ~2.3 waves per wave
+  // slot), the slowest tiles (long glass / metal paths) then set the frame
+  // time, so the chunks are split over `units` waves (tools/rank_times.py).
+  const int n_chunks = std::max(1, (prm->spp + RT_CHUNK_SPP - 1) / RT_CHUNK_SPP);
+  long long units = prm->units;
+  if (units <= 0) units = tiles < rtk::kSplitTiles ? n_chunks : 1;
+  if (prm->spp <= 0 || prm->max_depth <= 0) units = 1;  // nothing is traced
+  units = std::max(1LL, std::min<long long>(units, n_chunks));
+  const int cpu = (int)((n_chunks + units - 1) / units);
+  units = (n_chunks + cpu - 1) / cpu;
+  kp.n_chunks = n_chunks;
+  kp.units = (int)units;
+  kp.chunks_per_unit = cpu;
+  kp.chunk_stride = (uint64_t)prm->local_rows * (uint64_t)prm->width * 3u;
+  float *chunks = nullptr;
+  if (units > 1) {
+    const size_t need = (size_t)n_chunks * kp.chunk_stride;
+    if (need > c->chunk_floats) {
+      RT_HIP(hipStreamSynchronize(st));
+      (void)hipFree(c->d_chunks);
+      c->d_chunks = nullptr;
+      c->chunk_floats = 0;
+      RT_HIP(hipMalloc(&c->d_chunks, need * sizeof(float)));
+      c->chunk_floats = need;
+    }
+    chunks = c->d_chunks;
+  }
+  kLaunch[v]((unsigned)(blocks * units), st, kp, c, accum_rgb, chunks);
   RT_HIP(hipGetLastError());
+  if (units > 1) {
+    const uint64_t n = kp.chunk_stride;
+    const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, 256u * 64u);
+    rtk::fold_chunks<<<grid, 256, 0, st>>>(chunks, accum_rgb, cpu, n_chunks, n, prm->width, prm->height,
+                                           prm->row_block, prm->band_stride, prm->band_offset);
+    RT_HIP(hipGetLastError());
+  }
   return RT_OK;
 }
 
@@ -1095,6 +1186,7 @@ int rt_render(rt_context *c, const rt_camera *cam, const rt_params *prm, float *
   RT_HIP(hipSetDevice(c->device));
   if (nf > c->frame_floats) {
     (void)hipFree(c->d_frame);
+  (void)hipFree(c->d_chunks);
     c->d_frame = nullptr;
     c->frame_floats = 0;
     RT_HIP(hipMalloc(&c->d_frame, nf * sizeof(float)));

@@ -31,6 +31,7 @@ RT_FLAG_GPU_SEMANTICS = 3
 RT_FLAG_KEEP_COUNTERS = 1 << 8
 RT_FLAG_ACCEL_BVH = 1 << 9
 RT_FLAG_COUNT_WORK = 1 << 10
+RT_CHUNK_SPP = 64  # include/rt.h: samples per chunk of the two-level pixel sum
 
 _f = ctypes.POINTER(ctypes.c_float)
 _u32 = ctypes.POINTER(ctypes.c_uint32)
@@ -60,7 +61,7 @@ class Params(ctypes.Structure):
                 ("seed", ctypes.c_uint64), ("row_block", ctypes.c_int32),
                 ("band_stride", ctypes.c_int32), ("band_offset", ctypes.c_int32),
                 ("local_rows", ctypes.c_int32), ("flags", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("units", ctypes.c_uint32)]
 
 
 class Stats(ctypes.Structure):
@@ -214,14 +215,18 @@ def camera_gpu(width, height, lookfrom=(13, 2, 3), lookat=(0, 0, 0), vup=(0, 1, 
     return cam
 
 
-def make_params(width, height, spp, max_depth=50, seed=0, flags=0, rank=0, world=1, row_block=8):
-    """Params for rank `rank` of `world` (interleaved row bands of row_block rows)."""
+def make_params(width, height, spp, max_depth=50, seed=0, flags=0, rank=0, world=1, row_block=8,
+                units=0):
+    """Params for rank `rank` of `world` (interleaved row bands of row_block rows).
+
+    units: waves sharing each tile's sample chunks (0 = automatic); scheduling
+    only, the image is the same for every value (RT_CHUNK_SPP)."""
     if world == 1:
-        return Params(width, height, spp, max_depth, seed, max(1, height), 1, 0, height, flags, 0)
+        return Params(width, height, spp, max_depth, seed, max(1, height), 1, 0, height, flags, units)
     band_rows = row_block * world
     n_bands = -(-height // band_rows)  # every rank gets the same number of bands
     return Params(width, height, spp, max_depth, seed, row_block, world, rank, n_bands * row_block,
-                  flags, 0)
+                  flags, units)
 
 
 def local_to_global_rows(p):

@@ -209,3 +209,35 @@ def test_headline_geometry_one_spp(rtow, gpu_ctx):
     m_big = big.reshape(-1, 3).mean(0)
     m_small = small.reshape(-1, 3).mean(0) / 4
     assert np.all(np.abs(m_big - m_small) < 0.01), (m_big, m_small)
+
+
+@pytest.mark.parametrize("units", [1, 2, 3])
+def test_chunked_sum_bit_exact_vs_oracle(rtow, gpu_ctx, units, accel):
+    """spp > RT_CHUNK_SPP: three sample chunks (64, 64, 22), traced by 1, 2 or
+    3 waves per tile; the two-level sum matches the oracle bit for bit."""
+    scene = rtow.final_scene()
+    cam = rtow.camera_cpu(aspect=2.0)
+    p = rtow.make_params(24, 12, 150, seed=17, units=units)
+    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p, accel))
+
+
+def test_units_do_not_change_the_image(rtow, gpu_ctx):
+    """rt_params.units only schedules: 1..8 waves per tile and the automatic
+    choice, alone and combined with an 8-rank partition, give the same sums."""
+    gpu_ctx.upload(rtow.final_scene())
+    cam = rtow.camera_cpu(aspect=320 / 120)
+    bvh = rtow.RT_FLAG_ACCEL_BVH
+    ref, st = gpu_ctx.render(cam, rtow.make_params(320, 120, 500, seed=4, flags=bvh, units=1))
+    for u in (0, 2, 3, 5, 8):
+        got, st2 = gpu_ctx.render(cam, rtow.make_params(320, 120, 500, seed=4, flags=bvh, units=u))
+        assert np.array_equal(got, ref), u
+        assert st2.segments == st.segments
+    got = np.zeros_like(ref)
+    for rank in range(8):
+        p = rtow.make_params(320, 120, 500, seed=4, flags=bvh, rank=rank, world=8, units=8)
+        tile, _ = gpu_ctx.render(cam, p)
+        rows = rtow.local_to_global_rows(p)
+        keep = rows < 120
+        got[rows[keep]] = tile[keep]
+        assert not tile[~keep].any()
+    assert np.array_equal(got, ref)
