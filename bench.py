@@ -36,8 +36,18 @@ FLOPS_PER_TEST = 17           # algorithmic flops per ray-sphe
 FLOPS_PER_BOX = 12            # slab test: 6 fma (2 flop) per ray-box test (BVH mode)
 
 
+# BASELINE.json configs: (width, height, spp, half_extent of the sphere grid).  c2 is the
+# headline metric's config and the default; the others are for documentation
+# runs (`--preset c3` is what each of 8 GPUs renders 1/8 of, c4 is the
+# 10 000-sphere occupancy stress).
+PRESETS = {"c1": (1920, 1080, 100, 11), "c2": (3840, 2160, 500, 11),
+           "c3": (7680, 4320, 1000, 11), "c4": (16384, 16384, 2000, 50)}
+
+
 def parse():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--preset", choices=sorted(PRESETS), default="",
+                    help="BASELINE config (sets --width/--height/--spp/--half-extent)")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
@@ -56,7 +66,10 @@ def parse():
     ap.add_argument("--cpu-spp", type=int, default=30, help="spp of the bounded CPU sample (400x225)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--out", default="", help="write the gathered frame as PPM (P6 if .pgm/.p6)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.preset:
+        a.width, a.height, a.spp, a.half_extent = PRESETS[a.preset]
+    return a
 
 
 def cpu_baseline(spp):
@@ -121,6 +134,8 @@ def main():
 
     W, H, spp = a.width, a.height, a.spp
     workload = f"final random-spheres scene {W}x{H} @ {spp}spp depth {a.depth}"
+    if a.half_extent != 11:
+        workload += f", sphere grid half-extent {a.half_extent}"
     scene = rtow.final_scene(a.half_extent)
     cam = rtow.camera_cpu(aspect=W / H)
     ctx = rtow.Context(dev_idx)
@@ -210,7 +225,8 @@ def main():
         value = segments / elapsed / 1e6
         out = {
             "metric": "Mray/s (ray segments = closest-hit queries per second), final random-spheres "
-                      "scene 3840x2160 @ 500spp depth 50",
+                      "scene 3840x2160 @ 500spp depth 50" if not a.preset or a.preset == "c2"
+                      else f"Mray/s, {workload}",
             "value": round(value, 2),
             "unit": "Mray/s",
             "n_gpus": world,
