@@ -34,6 +34,9 @@ sys.path.insert(0, PKG)
 PEAK_FP32_TFLOPS = 157.3      # MI355X vector fp32 (MI355X_MICROARCH.md, chip table)
 FLOPS_PER_TEST = 17           # algorithmic flops per ray-sphere test
 FLOPS_PER_BOX = 12            # slab test: 6 fma (2 flop) per ray-box test (BVH mode)
+# wave64 VALU issue ceiling: one independent v_fma_f32 per 1.041 ns per SIMD
+# with all 64 lanes active (tools/ubench_exec.hip on MI355X), 256 CUs x 4 SIMDs
+VALU_ISSUE_PEAK = 1024 / 1.041e-9  # wave instructions per second
 
 
 # BASELINE.json configs: (width, height, spp, half_extent of the sphere grid).  c2 is the
@@ -93,18 +96,19 @@ def cpu_baseline(spp):
             "seconds": round(dt, 3), "sample": sample + " (oracle fp64 restatement)"}
 
 
-def load_traffic(workload, accel="scan"):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py)."""
+def load_pmc(workload, accel="scan"):
+    """The committed rocprofv3 PMC summary of this workload (tools/pmc_traffic.py):
+    HBM bytes and VALU wave-instructions per launch; {} if none matches."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json" if accel == "scan"
                         else f"pmc_traffic_{accel}.json")
     try:
         with open(path) as f:
             d = json.load(f)
         if d.get("workload") == workload:
-            return d.get("hbm_bytes_per_launch")
+            return d
     except (OSError, ValueError):
         pass
-    return None
+    return {}
 
 
 def main():
@@ -223,6 +227,8 @@ def main():
         achieved = flops / k_avg_s / 1e12
         bf_achieved = work.bf_tests * FLOPS_PER_TEST / k_avg_s / 1e12
         value = segments / elapsed / 1e6
+        pmc = load_pmc(workload, a.accel)
+        valu_insts = pmc.get("valu_insts_per_launch")
         out = {
             "metric": "Mray/s (ray segments = closest-hit queries per second), final random-spheres "
                       "scene 3840x2160 @ 500spp depth 50" if not a.preset or a.preset == "c2"
@@ -255,10 +261,19 @@ def main():
                                       "brute_force_equiv_tests": work.bf_tests},
             "roofline": {"bound": "valu", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                         "traffic": load_traffic(workload, a.accel),
+                         "traffic": pmc.get("hbm_bytes_per_launch"),
                          "brute_force_equiv_achieved": round(bf_achieved, 2),
+                         "valu_issue": ({"achieved": round(valu_insts / k_avg_s / 1e9, 1),
+                                         "peak": round(VALU_ISSUE_PEAK / 1e9, 1),
+                                         "unit": "G wave-instr/s",
+                                         "frac": round(valu_insts / k_avg_s / VALU_ISSUE_PEAK, 3),
+                                         "source": "SQ_INSTS_VALU per launch from the committed PMC "
+                                                   "summary / this run's kernel time"}
+                                        if valu_insts else None),
                          "note": "fp32 VALU-bound (no MFMA): executed ray-sphere tests x 17 flop "
-                                 "+ ray-box tests x 12 flop per launch / HIP-event kernel time"},
+                                 "+ ray-box tests x 12 flop per launch / HIP-event kernel time; "
+                                 "the kernel is control-heavy (min/max, compares, branches), so "
+                                 "valu_issue is the bound it actually runs against"},
         }
         if world == 1 and not a.no_cpu_baseline:
             try:

@@ -4,7 +4,9 @@
     python tools/pmc_traffic.py <dir with *_counter_collection.csv> [...] \
         --workload "<bench workload string>" --out profiles/pmc_traffic.json
 
-HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE
+Also records SQ_INSTS_VALU (wave instructions per launch) when an SQ pass is
+given, for bench.py's VALU issue-rate view.  HBM bytes per launch follow
+MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE
 are in KiB; on gfx950 FETCH_SIZE reads 1/2 of the bytes of a wide coalesced
 streaming read, so the read side is doubled (the render kernel's reads are
 scalar/gather loads of a 15 KB scene, so this is an upper bound); WRITE_SIZE
@@ -42,6 +44,8 @@ def main():
         out["write_bytes"] = avg["WRITE_SIZE"] * 1024
         out["hbm_bytes_per_launch"] = int(2 * out["fetch_bytes"] + out["write_bytes"])
         out["correction"] = "read side x2 (gfx950 FETCH_SIZE half-count), KiB -> bytes"
+    if "SQ_INSTS_VALU" in avg:
+        out["valu_insts_per_launch"] = int(avg["SQ_INSTS_VALU"])  # wave-level instructions
     s = json.dumps(out, indent=1, sort_keys=True)
     print(s)
     if a.out:
