@@ -13,8 +13,8 @@
 // Everything renders on the GPU through librtow.so; flags override defaults:
 //   --width N --height N --spp N --depth N --seed N --spheres K (grid half
 //   extent; 11 = reference, 50 = 10k spheres) --scene final|five
-//   --camera cpu|gpu --semantics cpu|gpu --gpus N --device N --out FILE --p6
-//   --quiet
+//   --camera cpu|gpu --semantics cpu|gpu --accel bvh|scan --gpus N --device N
+//   --out FILE --p6 --quiet
 #include <fcntl.h>
 #include <unistd.h>
 
@@ -40,6 +40,7 @@ struct options {
   std::string scene = "final";
   int camera = RT_CAMERA_CPU;
   unsigned flags = 0;
+  bool bvh = true;  // BVH walk (bit-identical to the scan)
   int gpus = 1, device = 0;
   std::string out;
   bool p6 = false, quiet = false;
@@ -58,7 +59,8 @@ void check(int st, const char *what) {
   std::fprintf(stderr,
                "usage: %s [--width N] [--height N] [--spp N] [--depth N] [--seed N]\n"
                "          [--spheres HALF_EXTENT] [--scene final|five] [--camera cpu|gpu]\n"
-               "          [--semantics cpu|gpu] [--gpus N] [--device N] [--out FILE] [--p6] [--quiet]\n",
+               "          [--semantics cpu|gpu] [--accel bvh|scan] [--gpus N] [--device N]\n"
+               "          [--out FILE] [--p6] [--quiet]\n",
                argv0);
   std::exit(2);
 }
@@ -100,6 +102,7 @@ int main(int argc, char **argv) {
     else if (a == "--scene") o.scene = next();
     else if (a == "--camera") o.camera = std::string(next()) == "gpu" ? RT_CAMERA_GPU : RT_CAMERA_CPU;
     else if (a == "--semantics") o.flags = std::string(next()) == "gpu" ? RT_FLAG_GPU_SEMANTICS : 0u;
+    else if (a == "--accel") o.bvh = std::string(next()) != "scan";
     else if (a == "--gpus") o.gpus = std::atoi(next());
     else if (a == "--device") o.device = std::atoi(next());
     else if (a == "--out") o.out = next();
@@ -161,7 +164,7 @@ int main(int argc, char **argv) {
     p.spp = o.spp;
     p.max_depth = o.depth;
     p.seed = o.seed;
-    p.flags = o.flags;
+    p.flags = o.flags | (o.bvh ? RT_FLAG_ACCEL_BVH : 0u);
     if (o.gpus == 1) {
       p.row_block = o.height;
       p.band_stride = 1;
