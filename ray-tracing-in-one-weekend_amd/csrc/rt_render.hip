@@ -95,6 +95,23 @@ struct kparams {
   uint64_t chunk_stride;  // floats per chunk plane (local_rows * width * 3)
 };
 
+// The kernel arguments, re-read from the kernarg segment (constant address
+// space: scalar loads that hit the scalar cache) at the rare places that need
+// camera constants, instead of holding them in SGPRs for the whole kernel.
+// The empty asm hides the pointer's invariance so the compiler cannot hoist
+// the loads back to the kernel entry; the word-wise copy keeps the address
+// space (unused words are dead).
+typedef const uint32_t __attribute__((address_space(4))) kword_c;
+__device__ __forceinline__ kparams kernargs() {
+  kword_c *q = (kword_c *)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(q));
+  kparams r;
+  uint32_t *w = reinterpret_cast<uint32_t *>(&r);
+#pragma unroll
+  for (unsigned i = 0; i < sizeof(kparams) / 4; ++i) w[i] = q[i];
+  return r;
+}
+
 // ---------------------------------------------------------------- RNG ----
 // pcg4d (Jarzynski & Olano, "Hash Functions for GPU Rendering", JCGT 2020):
 // a 4-D -> 4-D counter hash; one call gives the 4 uniforms a bounce needs.
@@ -606,13 +623,7 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
           accr = accg = accb = 0.0f;
         }
         if (sample < s_end) {
-          // camera constants are re-read from the kernel-argument segment
-          // here (scalar loads, cache hits) instead of being held in SGPRs
-          // for the whole kernel: the empty asm hides the pointer's
-          // invariance so the loads stay at this (only) use
-          const kparams *pk = (const kparams *)__builtin_amdgcn_kernarg_segment_ptr();
-          asm volatile("" : "+s"(pk));
-          camera_ray(*pk, pix, col, grow, sample, ox, oy, oz, dx, dy, dz);
+          camera_ray(kernargs(), pix, col, grow, sample, ox, oy, oz, dx, dy, dz);  // camera re-read
           ++sample;
           depth = 0;
           thr = thg = thb = 1.0f;
