@@ -186,10 +186,13 @@ int rt_camera_gpu(const double lookfrom[3], const double lookat[3],
 
 /* ---- device context ---- */
 int rt_context_create(int device_ordinal, rt_context **out);
+/* Waits for everything enqueued on the context's device, then frees. */
 void rt_context_destroy(rt_context *ctx);
 
-/* Copies the scene to the device (geometry padded for the scan kernel).
- * Replaces new_world<<<1,1>>> (src/gpu/main.cu:18-75). */
+/* Copies the scene to the device (scan records, BVH, shading records) and
+ * builds the BVH.  Replaces new_world<<<1,1>>> (src/gpu/main.cu:18-75).
+ * Synchronises the device first: renders still running on any stream keep
+ * the previous scene.  Centres must be finite, radii finite and non-zero. */
 int rt_scene_upload(rt_context *ctx, const rt_scene_view *scene);
 
 /* Enqueue the render kernel on `stream` (a hipStream_t, NULL = the context's

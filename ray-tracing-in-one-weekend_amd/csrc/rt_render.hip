@@ -1008,8 +1008,10 @@ int rt_context_create(int device_ordinal, rt_context **out) {
 
 void rt_context_destroy(rt_context *c) {
   if (!c) return;
-  if (c->device >= 0) (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->device >= 0) {
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();  // renders on caller streams may still use the buffers
+  }
   free_scene(c);
   (void)hipFree(c->d_counters);
   (void)hipFree(c->d_frame);
@@ -1025,7 +1027,8 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
                             !s->mat_param || !s->albedo_rgb)))
     return RT_ERR_INVALID;
   for (uint32_t i = 0; i < s->n; ++i)
-    if (s->mat_kind[i] > RT_DIELECTRIC || !(s->radius[i] != 0.0f) || !std::isfinite(s->radius[i]))
+    if (s->mat_kind[i] > RT_DIELECTRIC || !(s->radius[i] != 0.0f) || !std::isfinite(s->radius[i]) ||
+        !std::isfinite(s->cx[i]) || !std::isfinite(s->cy[i]) || !std::isfinite(s->cz[i]))
       return RT_ERR_INVALID;
   const uint32_t n = s->n;
   const uint32_t n_pad = (n + rtk::kSpherePad - 1) / rtk::kSpherePad * rtk::kSpherePad;
@@ -1059,6 +1062,8 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
   for (size_t k = 0; k < bb.slots.size(); ++k) fill_slot(bgeom[k / 2], (int)(k & 1), s, bb.slots[k]);
 
   RT_HIP(hipSetDevice(c->device));
+  // renders enqueued on caller streams may still read the old scene
+  RT_HIP(hipDeviceSynchronize());
   free_scene(c);
   hipError_t e = upload_vec(&c->d_geom, geom, c->stream);
   if (e == hipSuccess) e = upload_vec(&c->d_bvh_geom, bgeom, c->stream);
@@ -1143,7 +1148,7 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
   if (units > 1) {
     const size_t need = (size_t)n_chunks * kp.chunk_stride;
     if (need > c->chunk_floats) {
-      RT_HIP(hipStreamSynchronize(st));
+      RT_HIP(hipDeviceSynchronize());  // an earlier launch on any stream may still use it
       (void)hipFree(c->d_chunks);
       c->d_chunks = nullptr;
       c->chunk_floats = 0;

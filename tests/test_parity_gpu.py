@@ -261,3 +261,15 @@ def test_cli_bvh_and_scan_print_the_same_ppm(tmp_path):
     assert raw.startswith(head)
     vals = np.array(a.split()[4:], dtype=np.uint8)
     assert np.array_equal(np.frombuffer(raw[len(head):], np.uint8), vals)
+
+
+def test_scene_upload_rejects_non_finite_centres(rtow, gpu_ctx):
+    s = rtow.final_scene()
+    cx = s.cx.copy()
+    cx[5] = np.nan
+    bad = rtow.Scene(cx, s.cy, s.cz, s.radius, s.kind, s.albedo, s.param)
+    with pytest.raises(Exception, match="rt_scene_upload"):
+        gpu_ctx.upload(bad)
+    gpu_ctx.upload(s)  # the context stays usable
+    out, st = gpu_ctx.render(rtow.camera_cpu(aspect=2.0), rtow.make_params(16, 8, 1))
+    assert st.segments > 0
