@@ -845,12 +845,36 @@ struct bvh_builder {
     tree[id].right = r;
     return id;
   }
+  // Collapsed internal nodes get no box of their own: their children take
+  // their place in the DFS order (a wider tree; the stackless walk handles any
+  // arity).  A wave enters a node when ANY of its 64 rays meets the box, so
+  // node entry rates are high (60-94 % per level measured, tools/node_stats.py)
+  // and the box tests of nodes a wave almost always enters are wasted:
+  // collapsing X saves tests(X) and costs (tests(X) - enters(X)) per child.
+  // Rule: collapse the root and every internal node whose surface area is more
+  // than kCollapseArea of its nearest emitted ancestor's (461 ->
+  // 417 ms on the headline frame, neutral on the 10 000-sphere scene).  The
+  // walk stays conservative: a parent's box contains its children's.
+  static constexpr double kCollapseArea = 0.35;
+  bool collapsed(int t, int parent) const {
+    if (tree[t].leaf) return false;
+    if (t == 0) return true;  // the root (build() returns 0 for it): always entered
+    // the root's children have no emitted ancestor: they stay
+    return parent >= 0 && area(tree[t].b) > kCollapseArea * area(tree[parent].b);
+  }
   // DFS pre-order for octant oct (bit k set = direction negative along axis k):
   // a ray moving towards -axis meets the upper (right) child first
-  void emit(int t, int oct, size_t base) {
+  // (parent: nearest emitted ancestor, -1 at the root)
+  void emit(int t, int oct, size_t base, int parent = -1) {
+    const tnode &tn = tree[t];
+    if (collapsed(t, parent)) {
+      const bool neg = (oct >> tn.axis) & 1;
+      emit(neg ? tn.right : tn.left, oct, base, parent);
+      emit(neg ? tn.left : tn.right, oct, base, parent);
+      return;
+    }
     const size_t id = nodes.size();
     nodes.push_back(rtk::bvh_node{});
-    const tnode &tn = tree[t];
     if (tn.leaf) {
       rtk::bvh_node &nd = nodes[id];
       set_box(nd, tn.b);
@@ -859,8 +883,8 @@ struct bvh_builder {
       return;
     }
     const bool neg = (oct >> tn.axis) & 1;
-    emit(neg ? tn.right : tn.left, oct, base);
-    emit(neg ? tn.left : tn.right, oct, base);
+    emit(neg ? tn.right : tn.left, oct, base, t);
+    emit(neg ? tn.left : tn.right, oct, base, t);
     rtk::bvh_node &nd = nodes[id];
     set_box(nd, tn.b);
     nd.skip = (int32_t)(nodes.size() - base);
