@@ -57,7 +57,10 @@ def main():
             for k in kids:
                 walk(k, d + 1)
 
-        walk(0, 0)
+        i = 0  # the root may be collapsed: walk every top-level sibling
+        while i < n_nodes:
+            walk(i, 0)
+            i = skip[i]
     tot_t = sum(v[0] for v in by_depth.values())
     print(json.dumps({"frame": f"{w}x{h}x{spp}", "n_nodes_per_order": int(n_nodes), "wave_steps": steps,
                       "wave_tests_per_step": round(tot_t / steps, 2),
