@@ -117,7 +117,7 @@ typedef struct {
  * local_rows = height. */
 typedef struct {
   int32_t width, height;
-  int32_t spp, max_depth;
+  int32_t spp, max_depth; /* each < 2^24 (the RNG's counters) */
   uint64_t seed;
   int32_t row_block;
   int32_t band_stride;

@@ -116,10 +116,14 @@ __device__ __forceinline__ kparams kernargs() {
 // ---------------------------------------------------------------- RNG ----
 // pcg4d (Jarzynski & Olano, "Hash Functions for GPU Rendering", JCGT 2020):
 // a 4-D -> 4-D counter hash; one call gives the 4 uniforms a bounce needs.
+// The second and third inputs (sample index, bounce slot) are < 2^24
+// (params_ok bounds spp and max_depth), as is the LCG multiplier: their
+// products take the full-rate 24-bit multiply (v_mul_u32_u24, the same low
+// 32 bits) instead of the quarter-rate v_mul_lo_u32.
 __device__ __forceinline__ uint4 pcg4d(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   uint32_t x = a * 1664525u + 1013904223u;
-  uint32_t y = b * 1664525u + 1013904223u;
-  uint32_t z = c * 1664525u + 1013904223u;
+  uint32_t y = __umul24(b, 1664525u) + 1013904223u;
+  uint32_t z = __umul24(c, 1664525u) + 1013904223u;
   uint32_t w = d * 1664525u + 1013904223u;
   x += y * w; y += z * x; z += x * y; w += y * z;
   x ^= x >> 16; y ^= y >> 16; z ^= z >> 16; w ^= w >> 16;
@@ -727,7 +731,8 @@ int hip_fail(hipError_t e) {
   } while (0)
 
 bool params_ok(const rt_params *p) {
-  return p && p->width >= 1 && p->height >= 1 && p->spp >= 0 && p->max_depth >= 0 &&
+  return p && p->width >= 1 && p->height >= 1 && p->spp >= 0 && p->spp < (1 << 24) &&
+         p->max_depth >= 0 && p->max_depth < (1 << 24) &&
          p->row_block >= 1 && p->band_stride >= 1 && p->band_offset >= 0 &&
          p->band_offset < p->band_stride && p->local_rows >= 0 &&
          (uint64_t)p->width * (uint64_t)p->height < (1ull << 32);
