@@ -46,8 +46,11 @@ def main():
             ref = img
         else:
             same = bool(np.array_equal(ref, img))
-        print(json.dumps({"variant": v, "kernel_ms": [round(x, 3) for x in ms], "segments": st.segments,
-                          "identical_to_first": same}), flush=True)
+        import hashlib
+        print(json.dumps({"lib": os.path.basename(rtow.LIB_PATH), "variant": v,
+                          "kernel_ms": [round(x, 3) for x in ms], "segments": st.segments,
+                          "identical_to_first": same,
+                          "sha256": hashlib.sha256(img.tobytes()).hexdigest()[:16]}), flush=True)
 
 
 if __name__ == "__main__":

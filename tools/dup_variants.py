@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Experiment: marginal cost of one kernel component, measured by doing it TWICE.
+
+Builds build/variants/dup_<part>.so: the render kernel with one component
+computed a second time on asm-laundered inputs (the compiler cannot merge the
+copies) and its result consumed by an empty asm, so the image stays bit-identical
+(checked by tools/ab_flags.py's sha256) while the kernel time grows by what that
+component costs in place -- issue slots AND the latency it exposes.
+
+    python tools/dup_variants.py [part ...]     (default: all)
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "ray-tracing-in-one-weekend_amd", "csrc", "rt_render.hip")
+
+EDITS = {
+    # the ray-box slab test of every BVH node visit
+    "box": [("      if (__builtin_amdgcn_ballot_w64(tn <= tf)) {",
+             """      f2 vx2 = vix, vy2 = viy, vz2 = viz;
+      asm volatile("" : "+v"(vx2), "+v"(vy2), "+v"(vz2));
+      const f2 ux2 = fma2(nd.bx, vx2, vox), uy2 = fma2(nd.by, vy2, voy), uz2 = fma2(nd.bz, vz2, voz);
+      const float tn2 = fmaxf(fmaxf(fmaxf(fminf(ux2.x, ux2.y), fminf(uy2.x, uy2.y)), fminf(uz2.x, uz2.y)), 0.0f);
+      const float tf2 = fminf(fminf(fminf(fmaxf(ux2.x, ux2.y), fmaxf(uy2.x, uy2.y)), fmaxf(uz2.x, uz2.y)), hs.tmax);
+      asm volatile("" :: "v"(tn2), "v"(tf2));
+      if (__builtin_amdgcn_ballot_w64(tn <= tf)) {""")],
+    # the correctly rounded sqrt of each candidate sphere
+    "rootsqrt": [("    const float sq = sqrt_k(disc);\n    const float t0 = h - sq, t1 = h + sq;",
+                  """    const float sq = sqrt_k(disc);
+    float dd = disc;
+    asm volatile("" : "+v"(dd));
+    const float sq2 = sqrt_k(dd);
+    asm volatile("" :: "v"(sq2));
+    const float t0 = h - sq, t1 = h + sq;""")],
+    # the bounce's pcg4d
+    "pcg": [("        const uint4 r = pcg4d(pix, sample - 1u, (uint32_t)(depth + 1), p.seed32);",
+             """        const uint4 r = pcg4d(pix, sample - 1u, (uint32_t)(depth + 1), p.seed32);
+        uint32_t pq = pix;
+        asm volatile("" : "+v"(pq));
+        const uint4 r2 = pcg4d(pq, sample - 1u, (uint32_t)(depth + 1), p.seed32);
+        asm volatile("" :: "v"(r2.x), "v"(r2.y), "v"(r2.z));""")],
+    # sin/cos of the bounce's unit vector
+    "sincos": [("  sincos_turn(u2, s, c);\n  x = r * c;",
+                """  sincos_turn(u2, s, c);
+  float uu = u2, s2, c2;
+  asm volatile("" : "+v"(uu));
+  sincos_turn(uu, s2, c2);
+  asm volatile("" :: "v"(s2), "v"(c2));
+  x = r * c;""")],
+    # the winner's root refinement
+    "refine": [("        const float t = refine_root(sr, tmax, near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2);",
+                """        const float t = refine_root(sr, tmax, near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2);
+        float tq = tmax;
+        asm volatile("" : "+v"(tq));
+        const float t2 = refine_root(sr, tq, near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2);
+        asm volatile("" :: "v"(t2));""")],
+    # the camera ray of the next sample (path regeneration)
+    "camera": [("          camera_ray(kernargs(), pix, col, grow, sample, ox, oy, oz, dx, dy, dz);  // camera re-read",
+                """          camera_ray(kernargs(), pix, col, grow, sample, ox, oy, oz, dx, dy, dz);  // camera re-read
+          {
+            uint32_t sq = sample;
+            asm volatile("" : "+v"(sq));
+            float a0, a1, a2, a3, a4, a5;
+            camera_ray(kernargs(), pix, col, grow, sq, a0, a1, a2, a3, a4, a5);
+            asm volatile("" :: "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5));
+          }""")],
+}
+
+
+def main():
+    parts = sys.argv[1:] or list(EDITS)
+    src = open(SRC).read()
+    out = os.path.join(ROOT, "build", "variants")
+    os.makedirs(out, exist_ok=True)
+    for part in parts:
+        s = src
+        for old, new in EDITS[part]:
+            assert s.count(old) == 1, (part, old[:60])
+            s = s.replace(old, new)
+        d = os.path.join(out, "src_dup_" + part)
+        os.makedirs(d, exist_ok=True)
+        p = os.path.join(d, "rt_render.hip")
+        open(p, "w").write(s)
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
+                        "-ffp-contract=off", "-I" + os.path.join(ROOT, "include"),
+                        "-I" + os.path.join(ROOT, "ray-tracing-in-one-weekend_amd", "csrc"), "-shared",
+                        "-o", os.path.join(out, f"dup_{part}.so"), p,
+                        os.path.join(ROOT, "ray-tracing-in-one-weekend_amd", "csrc", "rt_host.cpp")],
+                       check=True)
+        print("built", f"dup_{part}.so")
+
+
+if __name__ == "__main__":
+    main()
