@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -479,9 +480,13 @@ __device__ __forceinline__ hit_state closest_hit(const kparams &p, const pair_ge
       const float tyl_n = fmaxf(fminf(tyl.x, tyl.y), 0.0f);
       const float tyl_f = fmaxf(tyl.x, tyl.y);
       float tyl_fc = fminf(tyl_f, hs.tmax);  // refreshed by walk_step after every leaf
-      int node = 0;
+      // a wave none of whose rays crosses the layer before tmax skips the walk
+      int node = __builtin_amdgcn_ballot_w64(tyl_n <= tyl_fc) ? 0 : p.n_nodes;
       while (node < p.n_nodes) {
         const bvh_node nd = order[node];
+        // by is unused here, but naming it keeps the node one s_load_dwordx8
+        // (else x2 + x4: 338 vs 342 ms)
+        asm volatile("" ::"s"(nd.by.x), "s"(nd.by.y));
         const f2 tx = fma2(nd.bx, vix, vox);
         const f2 tz = fma2(nd.bz, viz, voz);
         const float nx = fminf(tx.x, tx.y), fx = fmaxf(tx.x, tx.y);
@@ -809,10 +814,22 @@ struct bvh_builder {
   std::vector<rtk::bvh_node> nodes;
   std::vector<int> slots;          // slot -> original index, -1 padding
   static constexpr int kLeaf = 2 * rtk::kLeafPairs;
+  // tuning knobs, read once per build (A/B experiments; defaults measured best)
+  int max_leaf = env_int("RTOW_BVH_LEAF", kLeaf, 1, kLeaf);
+  double collapse_area = env_double("RTOW_BVH_COLLAPSE", 0.35);
+  double side_weight = env_double("RTOW_BVH_SIDE", 1.0);  // SAH weight of the x- and z-facing sides
+  static int env_int(const char *name, int dflt, int lo, int hi) {
+    const char *v = std::getenv(name);
+    return v ? std::max(lo, std::min(hi, std::atoi(v))) : dflt;
+  }
+  static double env_double(const char *name, double dflt) {
+    const char *v = std::getenv(name);
+    return v ? std::atof(v) : dflt;
+  }
 
-  static double area(const box &b) {
+  double area(const box &b) const {
     const double dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
-    return dx * dy + dy * dz + dz * dx;
+    return side_weight * (dx * dy + dy * dz) + dz * dx;
   }
   static void grow(box &a, const box &b) {
     for (int k = 0; k < 3; ++k) {
@@ -862,7 +879,7 @@ struct bvh_builder {
     for (uint32_t i = b; i < e; ++i) grow(all, sb[ord[i]]);
     tree[id].b = all;
     const uint32_t n = e - b;
-    if (n <= (uint32_t)kLeaf) {
+    if (n <= (uint32_t)max_leaf) {
       const uint32_t first_slot = (uint32_t)slots.size();
       const uint32_t width = n <= 2 ? 2u : (uint32_t)kLeaf;  // one pair or two
       for (uint32_t i = b; i < e; ++i) slots.push_back((int)ord[i]);
@@ -918,15 +935,15 @@ struct bvh_builder {
   // and the box tests of nodes a wave almost always enters are wasted:
   // collapsing X saves tests(X) and costs (tests(X) - enters(X)) per child.
   // Rule: collapse the root and every internal node whose surface area is more
-  // than kCollapseArea of its nearest emitted ancestor's (461 ->
+  // than collapse_area (0.35) of its nearest emitted ancestor's (461 ->
   // 417 ms on the headline frame, neutral on the 10 000-sphere scene).  The
   // walk stays conservative: a parent's box contains its children's.
-  static constexpr double kCollapseArea = 0.35;
+
   bool collapsed(int t, int parent) const {
     if (tree[t].leaf) return false;
     if (t == 0) return true;  // the root (build() returns 0 for it): always entered
     // the root's children have no emitted ancestor: they stay
-    return parent >= 0 && area(tree[t].b) > kCollapseArea * area(tree[parent].b);
+    return parent >= 0 && area(tree[t].b) > collapse_area * area(tree[parent].b);
   }
   // DFS pre-order for octant oct (bit k set = direction negative along axis k):
   // a ray moving towards -axis meets the upper (right) child first

@@ -273,3 +273,45 @@ def test_scene_upload_rejects_non_finite_centres(rtow, gpu_ctx):
     gpu_ctx.upload(s)  # the context stays usable
     out, st = gpu_ctx.render(rtow.camera_cpu(aspect=2.0), rtow.make_params(16, 8, 1))
     assert st.segments > 0
+
+
+def _with_extra_spheres(rtow, scene, spheres):
+    """scene + spheres [(x, y, z, r, kind, (r, g, b), param), ...] appended."""
+    import dataclasses
+    ex = list(zip(*spheres))
+    f32 = np.float32
+    return dataclasses.replace(
+        scene,
+        cx=np.concatenate([scene.cx, np.array(ex[0], f32)]),
+        cy=np.concatenate([scene.cy, np.array(ex[1], f32)]),
+        cz=np.concatenate([scene.cz, np.array(ex[2], f32)]),
+        radius=np.concatenate([scene.radius, np.array(ex[3], f32)]),
+        kind=np.concatenate([scene.kind, np.array(ex[4], np.uint32)]),
+        albedo=np.concatenate([scene.albedo, np.array(ex[5], f32).reshape(-1, 3)]),
+        param=np.concatenate([scene.param, np.array(ex[6], f32)]))
+
+
+@pytest.mark.parametrize("n_big", [12, 13])  # 4 + 12 = 16 spheres off the layer (layer mode), 17 (not)
+def test_bvh_layer_mode_boundary_bit_exact(rtow, gpu_ctx, n_big):
+    """Layer mode (the BVH over the thin layer of small spheres, the rest scanned
+    as pairs) and the plain BVH, on either side of its kMaxExtra = 16 limit, with
+    layer members of another radius inside the layer's y-range and a sphere that
+    pokes out of it: bit-exact vs the brute-force oracle, and BVH == scan."""
+    rng = np.random.default_rng(n_big)
+    extra = [(float(rng.uniform(-9, 9)), 1.0 + float(rng.uniform(0, 1)), float(rng.uniform(-9, 9)),
+              0.6 + 0.3 * float(rng.uniform()), i % 3, (0.7, 0.5, 0.3), 1.5 if i % 3 == 2 else 0.2)
+             for i in range(n_big - 1)]
+    extra += [(2.0, 0.25, 2.0, 0.2, 0, (0.9, 0.2, 0.2), 0.0)]     # pokes above the layer
+    extra += [(1.0, 0.2, -2.0, 0.15, 1, (0.8, 0.8, 0.8), 0.1),    # inside the layer's y-range
+              (-1.5, 0.2, 2.5, 0.1, 2, (1.0, 1.0, 1.0), 1.5)]
+    scene = _with_extra_spheres(rtow, rtow.final_scene(), extra)
+    cam = rtow.camera_cpu(aspect=96 / 54)
+    p = rtow.make_params(96, 54, 6, seed=9)
+    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p, ACCELS["bvh"]))
+    cam = rtow.camera_cpu(aspect=640 / 360)
+    p = rtow.make_params(640, 360, 8, seed=10)
+    a, sa = gpu_ctx.render(cam, p)
+    p.flags |= ACCELS["bvh"]
+    b, sb = gpu_ctx.render(cam, p)
+    assert sa.segments == sb.segments
+    assert np.array_equal(a, b)

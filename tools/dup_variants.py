@@ -18,14 +18,25 @@ SRC = os.path.join(ROOT, "ray-tracing-in-one-weekend_amd", "csrc", "rt_render.hi
 
 EDITS = {
     # the ray-box slab test of every BVH node visit
-    "box": [("      if (__builtin_amdgcn_ballot_w64(tn <= tf)) {",
-             """      f2 vx2 = vix, vy2 = viy, vz2 = viz;
-      asm volatile("" : "+v"(vx2), "+v"(vy2), "+v"(vz2));
-      const f2 ux2 = fma2(nd.bx, vx2, vox), uy2 = fma2(nd.by, vy2, voy), uz2 = fma2(nd.bz, vz2, voz);
-      const float tn2 = fmaxf(fmaxf(fmaxf(fminf(ux2.x, ux2.y), fminf(uy2.x, uy2.y)), fminf(uz2.x, uz2.y)), 0.0f);
-      const float tf2 = fminf(fminf(fminf(fmaxf(ux2.x, ux2.y), fmaxf(uy2.x, uy2.y)), fmaxf(uz2.x, uz2.y)), hs.tmax);
-      asm volatile("" :: "v"(tn2), "v"(tf2));
-      if (__builtin_amdgcn_ballot_w64(tn <= tf)) {""")],
+    "box": [("        node = walk_step<OPEN, STATS, true>(nd, node, tn <= tf, geom, orig, rp, hs, wc, tyl_f, tyl_fc);",
+             """        f2 vx2 = vix, vz2 = viz;
+        asm volatile("" : "+v"(vx2), "+v"(vz2));
+        const f2 ux2 = fma2(nd.bx, vx2, vox), uz2 = fma2(nd.bz, vz2, voz);
+        const float n2 = fmaxf(fmaxf(fminf(ux2.x, ux2.y), fminf(uz2.x, uz2.y)), tyl_n);
+        const float f2_ = fminf(fminf(fmaxf(ux2.x, ux2.y), fmaxf(uz2.x, uz2.y)), tyl_fc);
+        asm volatile("" :: "v"(n2), "v"(f2_));
+        node = walk_step<OPEN, STATS, true>(nd, node, tn <= tf, geom, orig, rp, hs, wc, tyl_f, tyl_fc);""")],
+    # the scan of the spheres off the layer (layer mode)
+    "extras": [("      if (STATS) wc.tests += 2 * p.n_extra_pairs;",
+                """      if (STATS) wc.tests += 2 * p.n_extra_pairs;
+      {
+        hit_state h2{__builtin_huge_valf(), -1, 1};
+        ray_pre r2 = rp;
+        asm volatile("" : "+v"(r2.dx), "+v"(r2.nk1));
+        for (int k = 0; k < p.n_extra_pairs; ++k)
+          scan_pairs<OPEN, 1, STATS>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, r2, h2, wc.roots);
+        asm volatile("" :: "v"(h2.tmax), "v"(h2.best));
+      }""")],
     # the correctly rounded sqrt of each candidate sphere
     "rootsqrt": [("    const float sq = sqrt_k(disc);\n    const float t0 = h - sq, t1 = h + sq;",
                   """    const float sq = sqrt_k(disc);
