@@ -65,7 +65,8 @@ struct __attribute__((aligned(32))) pair_geom {
 // not entered.  32 B = one s_load_dwordx8; the (lo, hi) pairs feed
 // v_pk_fma_f32 like the sphere records do.
 struct __attribute__((aligned(32))) bvh_node {
-  f2 bx, by, bz;  // (lo, hi) per axis
+  f2 bx, by, bz;  // (lo, hi) per axis; layer mode: bx = (centre x, centre z),
+                  // by = (half-width x, half-width z), bz unused (bvh_builder::to_centre_form)
   int32_t skip;
   uint32_t leaf;  // 0: internal (first child = this + 1); else (1 + first pair) | kTwoPairs
 };
@@ -458,8 +459,7 @@ __device__ __forceinline__ hit_state closest_hit(const kparams &p, const pair_ge
     const float ix = __builtin_amdgcn_rcpf(fabsf(dx) < 1e-18f ? copysignf(1e-18f, dx) : dx);
     const float iy = __builtin_amdgcn_rcpf(fabsf(dy) < 1e-18f ? copysignf(1e-18f, dy) : dy);
     const float iz = __builtin_amdgcn_rcpf(fabsf(dz) < 1e-18f ? copysignf(1e-18f, dz) : dz);
-    const f2 vix = {ix, ix}, viy = {iy, iy}, viz = {iz, iz};
-    const f2 vox = {-ox * ix, -ox * ix}, voy = {-oy * iy, -oy * iy}, voz = {-oz * iz, -oz * iz};
+    const float oix = -ox * ix, oiy = -oy * iy, oiz = -oz * iz;
     // the wave walks the DFS order of its majority direction octant, so
     // coherent rays visit near children first and tmax culls the rest
     const uint32_t half = __builtin_popcountll(__builtin_amdgcn_ballot_w64(true)) / 2;
@@ -474,32 +474,37 @@ __device__ __forceinline__ hit_state closest_hit(const kparams &p, const pair_ge
         scan_pairs<OPEN, 1, STATS>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, rp, hs, wc.roots);
       if (STATS) wc.tests += 2 * p.n_extra_pairs;
       // every node's y-range lies inside the layer's: its slab interval is
-      // computed once per ray, and a node tests x and z only (2 v_pk_fma_f32 +
-      // 7 VALU per box instead of 3 + 11)
-      const f2 tyl = fma2(p.layer, viy, voy);
+      // computed once per ray, and a node tests x and z only.  Nodes hold
+      // (centre, half-width) per axis: with m = (c - o) / d, the slab is
+      // m -+ h |1/d| whatever the sign of d, so x and z share the v_pk_fma_f32s
+      // and no min/max orders the slab ends (3 v_pk_fma_f32 + 3 VALU per box
+      // instead of 2 + 7)
+      const f2 tyl = fma2(p.layer, f2{iy, iy}, f2{oiy, oiy});
       const float tyl_n = fmaxf(fminf(tyl.x, tyl.y), 0.0f);
       const float tyl_f = fmaxf(tyl.x, tyl.y);
       float tyl_fc = fminf(tyl_f, hs.tmax);  // refreshed by walk_step after every leaf
       // a wave none of whose rays crosses the layer before tmax skips the walk
       int node = __builtin_amdgcn_ballot_w64(tyl_n <= tyl_fc) ? 0 : p.n_nodes;
+      const f2 vi = {ix, iz}, vo = {oix, oiz}, va = {fabsf(ix), fabsf(iz)};
       while (node < p.n_nodes) {
         const bvh_node nd = order[node];
-        // by is unused here, but naming it keeps the node one s_load_dwordx8
+        // bz is unused here, but naming it keeps the node one s_load_dwordx8
         // (else x2 + x4: 338 vs 342 ms)
-        asm volatile("" ::"s"(nd.by.x), "s"(nd.by.y));
-        const f2 tx = fma2(nd.bx, vix, vox);
-        const f2 tz = fma2(nd.bz, viz, voz);
-        const float nx = fminf(tx.x, tx.y), fx = fmaxf(tx.x, tx.y);
-        const float nz = fminf(tz.x, tz.y), fz = fmaxf(tz.x, tz.y);
+        asm volatile("" ::"s"(nd.bz.x), "s"(nd.bz.y));
+        const f2 m = fma2(nd.bx, vi, vo);
+        const f2 tn2 = fma2(-nd.by, va, m);
+        const f2 tf2 = fma2(nd.by, va, m);
         // v_max3 / v_min3 written out: fmaxf / fminf would first canonicalise
-        // the loop-carried operands (two extra v_max per node); the compare
-        // that follows needs no canonical input
+        // the loop-carried operands (extra v_max per node); the compare that
+        // follows needs no canonical input
         float tn, tf;
-        asm("v_max3_f32 %0, %1, %2, %3" : "=v"(tn) : "v"(nx), "v"(nz), "v"(tyl_n));
-        asm("v_min3_f32 %0, %1, %2, %3" : "=v"(tf) : "v"(fx), "v"(fz), "v"(tyl_fc));
+        asm("v_max3_f32 %0, %1, %2, %3" : "=v"(tn) : "v"(tn2.x), "v"(tn2.y), "v"(tyl_n));
+        asm("v_min3_f32 %0, %1, %2, %3" : "=v"(tf) : "v"(tf2.x), "v"(tf2.y), "v"(tyl_fc));
         node = walk_step<OPEN, STATS, true>(nd, node, tn <= tf, geom, orig, rp, hs, wc, tyl_f, tyl_fc);
       }
     } else {
+      const f2 vix = {ix, ix}, viy = {iy, iy}, viz = {iz, iz};
+      const f2 vox = {oix, oix}, voy = {oiy, oiy}, voz = {oiz, oiz};
       int node = 0;
       while (node < p.n_nodes) {
         const bvh_node nd = order[node];
@@ -973,6 +978,28 @@ struct bvh_builder {
     nd.skip = (int32_t)(nodes.size() - base);
     nd.leaf = 0;
   }
+  // Layer-mode node: the emitted x and z slabs [lo, hi] as (centre, half-width),
+  // bx = (cx, cz), by = (hx, hz).  The walk evaluates m = fma(c, 1/d, -o/d),
+  // m -+ fma(h, |1/d|): three roundings of magnitude <= (|o| + |c - o| + h) |1/d|
+  // against two for fma(lo, 1/d, -o/d), so h also covers |c - float(c)| and
+  // 2^-22 (3 oref + 2|c| + h) on top of the (lo, hi) padding.
+  void to_centre_form(rtk::bvh_node &nd) const {
+    float c[2], h[2];
+    const float lo[2] = {nd.bx[0], nd.bz[0]}, hi[2] = {nd.bx[1], nd.bz[1]};
+    for (int k = 0; k < 2; ++k) {
+      const double cd = 0.5 * ((double)lo[k] + (double)hi[k]);
+      const double hd = 0.5 * ((double)hi[k] - (double)lo[k]);
+      c[k] = (float)cd;
+      const double cover = hd + std::fabs(cd - (double)c[k]) +
+                           0x1p-22 * (3.0 * oref + 2.0 * std::fabs(cd) + hd);
+      h[k] = std::nextafter((float)cover, INFINITY);
+    }
+    nd.bx[0] = c[0];
+    nd.bx[1] = c[1];
+    nd.by[0] = h[0];
+    nd.by[1] = h[1];
+    nd.bz[0] = nd.bz[1] = 0.0f;
+  }
   size_t per_order = 0;
   // oref: the ray-origin bound the padding is valid for -- 64 or 16 beyond the
   // farthest sphere of radius <= 10, whichever is larger (the huge ground
@@ -1017,6 +1044,7 @@ struct bvh_builder {
       emit_axis(tree[0].b, 1, lo, hi);  // contains every node's y-range
       layer_lo = lo;
       layer_hi = hi;
+      for (rtk::bvh_node &nd : nodes) to_centre_form(nd);
       extra_pair0 = (uint32_t)slots.size() / 2;  // leaves end on a pair boundary
       for (uint32_t i = n_tree; i < n; ++i) slots.push_back((int)ord[i]);
       if (slots.size() & 1) slots.push_back(-1);
