@@ -101,6 +101,15 @@ struct kparams {
   // chunks [u*cpu, (u+1)*cpu) of its tiles, u = b % units, cpu = chunks_per_unit
   int n_chunks, units, chunks_per_unit, pad_;
   uint64_t chunk_stride;  // floats per chunk plane (local_rows * width * 3)
+  // device buffers (rt_context; out = the caller's frame tile)
+  const struct pair_geom *scan_geom;  // brute-force order
+  const struct pair_geom *geom;       // BVH leaf order
+  const struct bvh_node *nodes;       // 8 DFS orders of n_nodes
+  const int *orig;                    // BVH slot -> original index
+  const struct shade_rec *shade;
+  float *out;
+  float *chunks;
+  unsigned long long *counters;
 };
 
 // The kernel arguments, re-read from the kernarg segment (constant address
@@ -110,6 +119,36 @@ struct kparams {
 // the loads back to the kernel entry; the word-wise copy keeps the address
 // space (unused words are dead).
 typedef const uint32_t __attribute__((address_space(4))) kword_c;
+// Scene data are read-only for the whole launch: read through the constant
+// address space, uniform addresses become scalar (SMEM) loads into SGPRs.
+#define RT_CONST __attribute__((address_space(4)))
+template <class T>
+__device__ __forceinline__ const RT_CONST T *as_const(const T *p) {
+  return (const RT_CONST T *)p;
+}
+// per-lane buffers (shading records, frame, chunk sums, counters) in the global
+// address space: global_load/store rather than flat (no lgkmcnt coupling)
+#define RT_GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ RT_GLOBAL T *as_global(T *p) {
+  return (RT_GLOBAL T *)p;
+}
+// a whole record from the constant address space (one s_load_dwordxN when uniform)
+template <class T>
+__device__ __forceinline__ T cload_g(const RT_GLOBAL T *p) {
+  static_assert(sizeof(T) % 16 == 0, "16-byte records");
+  typedef uint32_t quad __attribute__((ext_vector_type(4)));
+  struct { quad q[sizeof(T) / 16]; } w;
+#pragma unroll
+  for (unsigned i = 0; i < sizeof(T) / 16; ++i) w.q[i] = ((const RT_GLOBAL quad *)p)[i];
+  return __builtin_bit_cast(T, w);
+}
+template <class T>
+__device__ __forceinline__ T cload(const RT_CONST T *p) {
+  static_assert(sizeof(T) % 4 == 0, "dword records");
+  typedef uint32_t words __attribute__((ext_vector_type(sizeof(T) / 4)));
+  return __builtin_bit_cast(T, *(const RT_CONST words *)p);
+}
 __device__ __forceinline__ kparams kernargs() {
   kword_c *q = (kword_c *)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(q));
@@ -312,8 +351,8 @@ struct ray_pre {
 // lane needs the sqrt / interval work.  orig maps slots to original indices
 // (BVH order); nullptr = identity (brute-force order).
 template <bool OPEN, int NP, bool STATS>
-__device__ __forceinline__ void scan_pairs(const pair_geom *__restrict__ g, int slot0,
-                                           const int *__restrict__ orig, const ray_pre &r,
+__device__ __forceinline__ void scan_pairs(const RT_CONST pair_geom *__restrict__ g, int slot0,
+                                           const RT_CONST int *__restrict__ orig, const ray_pre &r,
                                            hit_state &hs, uint32_t &roots) {
   pair_geom q[NP];
   f2 h[NP], e[NP];
@@ -321,7 +360,7 @@ __device__ __forceinline__ void scan_pairs(const pair_geom *__restrict__ g, int 
   uint64_t any = 0;
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
-    q[j] = g[j];
+    q[j] = cload(g + j);
     h[j] = fma2(q[j].cz, r.dz, fma2(q[j].cy, r.dy, fma2(q[j].cx, r.dx, r.nk1)));
     const f2 gg = fma2(q[j].cz, r.oz2, fma2(q[j].cy, r.oy2, fma2(q[j].cx, r.ox2, r.o2)));
     e[j] = fma2(h[j], h[j], -gg);
@@ -403,7 +442,8 @@ struct work_ctr {
 // combined far limit).
 template <bool OPEN, bool STATS, bool LAYER>
 __device__ __forceinline__ int walk_step(const bvh_node &nd, int node, bool hit,
-                                         const pair_geom *__restrict__ geom, const int *__restrict__ orig,
+                                         const RT_CONST pair_geom *__restrict__ geom,
+                                         const RT_CONST int *__restrict__ orig,
                                          const ray_pre &rp, hit_state &hs, work_ctr &wc, float lim_src,
                                          float &lim) {
   if (STATS) {
@@ -428,12 +468,17 @@ __device__ __forceinline__ int walk_step(const bvh_node &nd, int node, bool hit,
 // Closest hit of the ray (o, d) over all spheres: hittable_list::hit,
 // src/cpu/hittable_list.h:28-43.  Wave-uniform: every active lane of the wave
 // calls it together; the result does not depend on which lanes those are.
+// The scene parameters are re-read from the kernarg segment on entry
+// (kernargs()): they live in SGPRs for the walk only, not across the whole
+// bounce loop (SGPR pressure).
 template <bool OPEN, bool BVH, bool STATS>
-__device__ __forceinline__ hit_state closest_hit(const kparams &p, const pair_geom *__restrict__ scan_geom,
-                                                 const pair_geom *__restrict__ geom,
-                                                 const bvh_node *__restrict__ nodes,
-                                                 const int *__restrict__ orig, float ox, float oy, float oz,
-                                                 float dx, float dy, float dz, work_ctr &wc) {
+__device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, float dx, float dy, float dz,
+                                                 work_ctr &wc) {
+  const kparams p = kernargs();
+  const RT_CONST pair_geom *__restrict__ scan_geom = as_const(p.scan_geom);
+  const RT_CONST pair_geom *__restrict__ geom = as_const(p.geom);
+  const RT_CONST bvh_node *__restrict__ nodes = as_const(p.nodes);
+  const RT_CONST int *__restrict__ orig = as_const(p.orig);
   const int n_pairs = p.n_pad / 2;
   const float nk1 = -dot3(ox, oy, oz, dx, dy, dz);
   const float o2 = dot3(ox, oy, oz, ox, oy, oz);
@@ -466,7 +511,7 @@ __device__ __forceinline__ hit_state closest_hit(const kparams &p, const pair_ge
     const int oct = (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dx < 0.0f)) > half ? 1 : 0) |
                     (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dy < 0.0f)) > half ? 2 : 0) |
                     (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dz < 0.0f)) > half ? 4 : 0);
-    const bvh_node *__restrict__ order = nodes + (size_t)oct * p.n_nodes;
+    const RT_CONST bvh_node *__restrict__ order = nodes + (size_t)oct * p.n_nodes;
     if (p.layer_mode) {
       // the spheres off the layer (in the final scene the ground and the three
       // big spheres) are scanned first: their hits shorten tmax for the walk
@@ -487,7 +532,7 @@ __device__ __forceinline__ hit_state closest_hit(const kparams &p, const pair_ge
       int node = __builtin_amdgcn_ballot_w64(tyl_n <= tyl_fc) ? 0 : p.n_nodes;
       const f2 vi = {ix, iz}, vo = {oix, oiz}, va = {fabsf(ix), fabsf(iz)};
       while (node < p.n_nodes) {
-        const bvh_node nd = order[node];
+        const bvh_node nd = cload(order + node);
         // bz is unused here, but naming it keeps the node one s_load_dwordx8
         // (else x2 + x4: 338 vs 342 ms)
         asm volatile("" ::"s"(nd.bz.x), "s"(nd.bz.y));
@@ -507,7 +552,7 @@ __device__ __forceinline__ hit_state closest_hit(const kparams &p, const pair_ge
       const f2 vox = {oix, oix}, voy = {oiy, oiy}, voz = {oiz, oiz};
       int node = 0;
       while (node < p.n_nodes) {
-        const bvh_node nd = order[node];
+        const bvh_node nd = cload(order + node);
         const f2 tx = fma2(nd.bx, vix, vox);
         const f2 ty = fma2(nd.by, viy, voy);
         const f2 tz = fma2(nd.bz, viz, voz);
@@ -521,19 +566,16 @@ __device__ __forceinline__ hit_state closest_hit(const kparams &p, const pair_ge
   return hs;
 }
 
-// 7 waves per SIMD: the register budget that admits it (<= 72 VGPRs, SGPRs
-// for 7 blocks/CU) measured 3.6 % faster than the unconstrained 6-wave build
-// and much faster than forcing 8 (scratch spills).
+// 8 waves per SIMD (<= 64 VGPRs, 78 SGPRs).  The walk is a serial latency
+// chain per wave (scalar node load -> slab test -> ballot -> branch), so more
+// resident waves keep the VALU busier: 312 vs 322 ms at 7 waves, although the
+// 8-wave budget spills a few per-step values (none inside the walk).  That
+// became possible once the scene pointers and parameters were re-read from
+// the kernarg segment where they are used (kernargs(), as_const()) instead of
+// being held in SGPRs for the whole kernel: 94 SGPRs + 21 spilled -> 69 at 7
+// waves.
 template <bool OPEN, bool METAL_UNIT, bool BVH, bool STATS>
-__global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
-                                                        const pair_geom *__restrict__ scan_geom,
-                                                        const pair_geom *__restrict__ geom,
-                                                        const bvh_node *__restrict__ nodes,
-                                                        const int *__restrict__ orig,
-                                                        const shade_rec *__restrict__ shade,
-                                                        float *__restrict__ out,
-                                                        float *__restrict__ chunks,
-                                                        unsigned long long *__restrict__ counters) {
+__global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   const int lane = threadIdx.x & 63;
   const int unit = (int)(blockIdx.x % (unsigned)p.units);
   const int tile = (int)(blockIdx.x / (unsigned)p.units) * kWavesPerBlock + (threadIdx.x >> 6);
@@ -570,10 +612,11 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
   while (true) {
     hit_state hs{__builtin_huge_valf(), -1, 1};
     if (!__ballot(alive)) break;
-    if (alive) hs = closest_hit<OPEN, BVH, STATS>(p, scan_geom, geom, nodes, orig, ox, oy, oz, dx, dy, dz, wc);
+    if (alive) hs = closest_hit<OPEN, BVH, STATS>(ox, oy, oz, dx, dy, dz, wc);
     ++steps;
     if (alive) {
       ++segs;
+      const kparams q = kernargs();  // shading's parameters, re-read per step
       const float o2 = dot3(ox, oy, oz, ox, oy, oz);
       const float ox2 = -2.0f * ox, oy2 = -2.0f * oy, oz2 = -2.0f * oz;
       const float tmax = hs.tmax;
@@ -590,7 +633,7 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
         accb = fmaf(thb, s0 + a, accb);
         path_done = true;
       } else {
-        const shade_rec sr = shade[best];
+        const shade_rec sr = cload_g(as_global(q.shade) + best);
         const float t = refine_root(sr, tmax, near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2);
         const float px = fmaf(t, dx, ox), py = fmaf(t, dy, oy), pz = fmaf(t, dz, oz);
         float nx = (px - sr.cx) * sr.inv_r, ny = (py - sr.cy) * sr.inv_r, nz = (pz - sr.cz) * sr.inv_r;
@@ -603,7 +646,7 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
           ny = -ny;
           nz = -nz;
         }
-        const uint4 r = pcg4d(pix, sample - 1u, (uint32_t)(depth + 1), p.seed32);
+        const uint4 r = pcg4d(pix, sample - 1u, (uint32_t)(depth + 1), q.seed32);
         // shared by the material branches (computed once: lanes of one wave
         // usually hit several materials, so the branches all execute)
         const float dn = dot3(dx, dy, dz, nx, ny, nz);
@@ -660,7 +703,7 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
         thg *= sr.ag;
         thb *= sr.ab;
         ++depth;
-        if (!scattered || depth >= p.max_depth) {
+        if (!scattered || depth >= q.max_depth) {
           path_done = true;  // absorbed, or bounce limit (main.cc:16-17): black
         } else {
           ox = px;
@@ -679,8 +722,8 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
             s_tot[1][threadIdx.x] += accg;
             s_tot[2][threadIdx.x] += accb;
           } else {
-            float *c = chunks + (size_t)((sample - 1) / RT_CHUNK_SPP) * p.chunk_stride +
-                       3 * ((size_t)lrow * p.width + col);
+            RT_GLOBAL float *c = as_global(q.chunks) + (size_t)((sample - 1) / RT_CHUNK_SPP) * q.chunk_stride +
+                       3 * ((size_t)lrow * q.width + col);
             c[0] = accr;
             c[1] = accg;
             c[2] = accb;
@@ -700,7 +743,8 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
   }
 
   if (in_tile && unit == 0) {  // padding pixels (row >= height) write zeros
-    float *o = out + 3 * ((size_t)lrow * p.width + col);
+    const kparams q = kernargs();
+    RT_GLOBAL float *o = as_global(q.out) + 3 * ((size_t)lrow * q.width + col);
     o[0] = s_tot[0][threadIdx.x];
     o[1] = s_tot[1][threadIdx.x];
     o[2] = s_tot[2][threadIdx.x];
@@ -719,6 +763,7 @@ __global__ __launch_bounds__(kBlock, 7) void render_kernel(const kparams p,
     }
   }
   if (lane == 0) {
+    unsigned long long *counters = kernargs().counters;  // (4 atomics per wave)
     atomicAdd(&counters[0], (unsigned long long)s);
     atomicAdd(&counters[1], (unsigned long long)steps);
     if (STATS) {
@@ -1112,9 +1157,17 @@ void fill_slot(rtk::pair_geom &g, int l, const rt_scene_view *s, int i) {
 }
 
 template <bool O, bool U, bool B, bool S>
-void launch(unsigned blocks, hipStream_t st, const rtk::kparams &kp, rt_context *c, float *out, float *chunks) {
-  rtk::render_kernel<O, U, B, S><<<blocks, rtk::kBlock, 0, st>>>(
-      kp, c->d_geom, c->d_bvh_geom, c->d_nodes, c->d_orig, c->d_shade, out, chunks, c->d_counters);
+void launch(unsigned blocks, hipStream_t st, const rtk::kparams &kp0, rt_context *c, float *out, float *chunks) {
+  rtk::kparams kp = kp0;
+  kp.scan_geom = c->d_geom;
+  kp.geom = c->d_bvh_geom;
+  kp.nodes = c->d_nodes;
+  kp.orig = c->d_orig;
+  kp.shade = c->d_shade;
+  kp.out = out;
+  kp.chunks = chunks;
+  kp.counters = c->d_counters;
+  rtk::render_kernel<O, U, B, S><<<blocks, rtk::kBlock, 0, st>>>(kp);
 }
 
 using launch_fn = void (*)(unsigned, hipStream_t, const rtk::kparams &, rt_context *, float *, float *);
