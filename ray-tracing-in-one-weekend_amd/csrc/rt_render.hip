@@ -97,6 +97,8 @@ struct kparams {
   int layer_mode, extra_pair0, n_extra_pairs, pad2_;
   uint32_t seed32, flags;
   float inv_wm1, inv_hm1;  // 1/(W-1), 1/(H-1) rounded once (cpu camera model)
+  // exact division by the width: W = wodd << wshift, wodd * winv == 1 (mod 2^32)
+  uint32_t wshift, winv;
   // sample chunks (RT_CHUNK_SPP) and their split over waves: block b traces
   // chunks [u*cpu, (u+1)*cpu) of its tiles, u = b % units, cpu = chunks_per_unit
   int n_chunks, units, chunks_per_unit, pad_;
@@ -566,6 +568,14 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
   return hs;
 }
 
+// This lane's index in its wave, recomputed where it is needed (volatile: not
+// hoisted, so it is not held in a VGPR through the bounce loop).
+__device__ __forceinline__ int lane_now() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 // 8 waves per SIMD (<= 64 VGPRs, 78 SGPRs).  The walk is a serial latency
 // chain per wave (scalar node load -> slab test -> ballot -> branch), so more
 // resident waves keep the VALU busier: 312 vs 322 ms at 7 waves, although the
@@ -576,18 +586,25 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
 // waves.
 template <bool OPEN, bool METAL_UNIT, bool BVH, bool STATS>
 __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
-  const int lane = threadIdx.x & 63;
+  // Per-lane values that the bounce loop rarely needs are not kept live (VGPR
+  // pressure at 8 waves): the wave keeps its tile origin (col0, lrow0, SGPRs)
+  // and the lane its global pixel index; column, row and the s_tot slot are
+  // recomputed from lane_now() where they are used.
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x) >> 6;
   const int unit = (int)(blockIdx.x % (unsigned)p.units);
-  const int tile = (int)(blockIdx.x / (unsigned)p.units) * kWavesPerBlock + (threadIdx.x >> 6);
-  const int tx = tile % p.tiles_x, ty = tile / p.tiles_x;
-  const int col = tx * kTile + (lane & (kTile - 1));
-  const int lrow = ty * kTile + (lane >> 3);
-  const int band = lrow / p.row_block;
-  const int grow = (band * p.band_stride + p.band_offset) * p.row_block + (lrow - band * p.row_block);
-  const bool in_tile = col < p.width && lrow < p.local_rows;
-  const bool valid = in_tile && grow < p.height;
-  const uint32_t pix = (uint32_t)grow * (uint32_t)p.width + (uint32_t)col;
-
+  const int tile = (int)(blockIdx.x / (unsigned)p.units) * kWavesPerBlock + wave;
+  const int col0 = (tile % p.tiles_x) * kTile, lrow0 = (tile / p.tiles_x) * kTile;
+  uint32_t pix;
+  bool valid;
+  {
+    const int lane = lane_now();
+    const int col = col0 + (lane & (kTile - 1));
+    const int lrow = lrow0 + (lane >> 3);
+    const int band = lrow / p.row_block;
+    const int grow = (band * p.band_stride + p.band_offset) * p.row_block + (lrow - band * p.row_block);
+    valid = col < p.width && lrow < p.local_rows && grow < p.height;
+    pix = (uint32_t)grow * (uint32_t)p.width + (uint32_t)col;
+  }
   float accr = 0.f, accg = 0.f, accb = 0.f;
   float ox = 0.f, oy = 0.f, oz = 0.f, dx = 0.f, dy = 1.f, dz = 0.f;
   float thr = 1.f, thg = 1.f, thb = 1.f;
@@ -603,8 +620,16 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   // fold_chunks
   __shared__ float s_tot[3][kBlock];
   s_tot[0][threadIdx.x] = s_tot[1][threadIdx.x] = s_tot[2][threadIdx.x] = 0.0f;
+  // (col, global row) of this lane's pixel from pix: col from the tile origin,
+  // row by exact division (pix - col) / W
+  auto pixel_cr = [&](const kparams &k, int &col, int &grow) {
+    col = col0 + (lane_now() & (kTile - 1));
+    grow = (int)(((pix - (uint32_t)col) >> k.wshift) * k.winv);
+  };
   bool alive = valid && s_end > s_begin && p.max_depth > 0;  // depth 0: black, no hit test
   if (alive) {
+    int col, grow;
+    pixel_cr(p, col, grow);
     camera_ray(p, pix, col, grow, s_begin, ox, oy, oz, dx, dy, dz);
     sample = s_begin + 1;
   }
@@ -717,11 +742,14 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
       }
       if (path_done) {
         if (sample % RT_CHUNK_SPP == 0 || sample == s_end) {  // the path closed a chunk
+          const int l = lane_now();
           if (unit == 0) {
-            s_tot[0][threadIdx.x] += accr;
-            s_tot[1][threadIdx.x] += accg;
-            s_tot[2][threadIdx.x] += accb;
+            const int slot = wave * 64 + l;
+            s_tot[0][slot] += accr;
+            s_tot[1][slot] += accg;
+            s_tot[2][slot] += accb;
           } else {
+            const int col = col0 + (l & (kTile - 1)), lrow = lrow0 + (l >> 3);
             RT_GLOBAL float *c = as_global(q.chunks) + (size_t)((sample - 1) / RT_CHUNK_SPP) * q.chunk_stride +
                        3 * ((size_t)lrow * q.width + col);
             c[0] = accr;
@@ -731,7 +759,10 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           accr = accg = accb = 0.0f;
         }
         if (sample < s_end) {
-          camera_ray(kernargs(), pix, col, grow, sample, ox, oy, oz, dx, dy, dz);  // camera re-read
+          const kparams k = kernargs();  // camera re-read
+          int col, grow;
+          pixel_cr(k, col, grow);
+          camera_ray(k, pix, col, grow, sample, ox, oy, oz, dx, dy, dz);
           ++sample;
           depth = 0;
           thr = thg = thb = 1.0f;
@@ -742,12 +773,17 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
     }
   }
 
-  if (in_tile && unit == 0) {  // padding pixels (row >= height) write zeros
+  const int lane = lane_now();
+  if (unit == 0) {
     const kparams q = kernargs();
-    RT_GLOBAL float *o = as_global(q.out) + 3 * ((size_t)lrow * q.width + col);
-    o[0] = s_tot[0][threadIdx.x];
-    o[1] = s_tot[1][threadIdx.x];
-    o[2] = s_tot[2][threadIdx.x];
+    const int col = col0 + (lane & (kTile - 1)), lrow = lrow0 + (lane >> 3);
+    if (col < q.width && lrow < q.local_rows) {  // padding pixels (row >= height) write zeros
+      RT_GLOBAL float *o = as_global(q.out) + 3 * ((size_t)lrow * q.width + col);
+      const int slot = wave * 64 + lane;
+      o[0] = s_tot[0][slot];
+      o[1] = s_tot[1][slot];
+      o[2] = s_tot[2][slot];
+    }
   }
   // one atomic per wave for the counters
   uint32_t s = segs;
@@ -1374,6 +1410,17 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
   kp.flags = prm->flags;
   kp.inv_wm1 = (float)(1.0 / (prm->width - 1));
   kp.inv_hm1 = (float)(1.0 / (prm->height - 1));
+  {
+    uint32_t w = (uint32_t)prm->width, sh = 0;
+    while (!(w & 1u)) {
+      w >>= 1;
+      ++sh;
+    }
+    uint32_t inv = w;  // Newton: inv = inv (2 - w inv) doubles the correct low bits
+    for (int k = 0; k < 5; ++k) inv *= 2u - w * inv;
+    kp.wshift = sh;
+    kp.winv = inv;
+  }
   const int tiles_y = (prm->local_rows + rtk::kTile - 1) / rtk::kTile;
   const long long tiles = (long long)kp.tiles_x * tiles_y;
   const unsigned blocks = (unsigned)((tiles + rtk::kWavesPerBlock - 1) / rtk::kWavesPerBlock);
