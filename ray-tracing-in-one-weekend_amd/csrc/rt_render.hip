@@ -517,8 +517,8 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
     if (p.layer_mode) {
       // the spheres off the layer (in the final scene the ground and the three
       // big spheres) are scanned first: their hits shorten tmax for the walk
-      for (int k = 0; k < p.n_extra_pairs; ++k)
-        scan_pairs<OPEN, 1, STATS>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, rp, hs, wc.roots);
+      for (int k = 0; k < p.n_extra_pairs; k += 2)
+        scan_pairs<OPEN, 2, STATS>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, rp, hs, wc.roots);
       if (STATS) wc.tests += 2 * p.n_extra_pairs;
       // every node's y-range lies inside the layer's: its slab interval is
       // computed once per ray, and a node tests x and z only.  Nodes hold
@@ -1128,7 +1128,9 @@ struct bvh_builder {
       for (rtk::bvh_node &nd : nodes) to_centre_form(nd);
       extra_pair0 = (uint32_t)slots.size() / 2;  // leaves end on a pair boundary
       for (uint32_t i = n_tree; i < n; ++i) slots.push_back((int)ord[i]);
-      if (slots.size() & 1) slots.push_back(-1);
+      // padded to whole groups of two pairs: the kernel scans them two at a
+      // time (one s_load_dwordx16, two independent chains)
+      while ((slots.size() - 2 * extra_pair0) % 4) slots.push_back(-1);
       n_extra_pairs = (uint32_t)slots.size() / 2 - extra_pair0;
     }
   }
