@@ -430,8 +430,8 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
         std::fprintf(g_trace, "seg %d O=(%.9g %.9g %.9g) D=(%.9g %.9g %.9g) |O|^2=%.9g\n", depth, o[0],
                      o[1], o[2], d[0], d[1], d[2], o2);
       for (size_t i = 0; i < n; ++i) {
-        const float h = fmaf_(sc.cz[i], d[2], fmaf_(sc.cy[i], d[1], fmaf_(sc.cx[i], d[0], nk1)));
-        const float g = fmaf_(sc.cz[i], oz2, fmaf_(sc.cy[i], oy2, fmaf_(sc.cx[i], ox2, o2)));
+        const float h = fmaf_(sc.cz[i], d[2], fmaf_(sc.cx[i], d[0], fmaf_(sc.cy[i], d[1], nk1)));
+        const float g = fmaf_(sc.cz[i], oz2, fmaf_(sc.cx[i], ox2, fmaf_(sc.cy[i], oy2, o2)));
         const float e = fmaf_(h, h, -g);
         if (e >= sc.ks[i]) {
           // sphere.h:34-44: the root offered is t0 if past t_min, else t1; it

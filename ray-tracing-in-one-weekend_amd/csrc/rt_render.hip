@@ -94,7 +94,8 @@ struct kparams {
   // one thin y-layer, whose slab interval the walk computes once per ray;
   // the few other spheres are n_extra_pairs scan pairs from extra_pair0 on
   f2 layer;
-  int layer_mode, extra_pair0, n_extra_pairs, pad2_;
+  int layer_mode, extra_pair0, n_extra_pairs;
+  float layer_cy;
   uint32_t seed32, flags;
   float inv_wm1, inv_hm1;  // 1/(W-1), 1/(H-1) rounded once (cpu camera model)
   // exact division by the width: W = wodd << wshift, wodd * winv == 1 (mod 2^32)
@@ -268,11 +269,10 @@ __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, fl
 }
 
 // camera ray for (pixel, sample): get_ray, src/cpu/camera.h:28-34 (model CPU)
-// or src/gpu/camera.h:153-167 (model GPU)
-__device__ __forceinline__ void camera_ray(const kparams &p, uint32_t pix, int col, int grow,
-                                           uint32_t sample, float &ox, float &oy, float &oz,
+// or src/gpu/camera.h:153-167 (model GPU); r = pcg4d(pix, sample, 0, seed32)
+__device__ __forceinline__ void camera_ray(const kparams &p, const uint4 r, int col, int grow,
+                                           float &ox, float &oy, float &oz,
                                            float &dx, float &dy, float &dz) {
-  uint4 r = pcg4d(pix, sample, 0u, p.seed32);
   float u1 = unif(r.x), u2 = unif(r.y);
   float fs, ft;
   if (p.cam.model == RT_CAMERA_CPU) {
@@ -352,7 +352,11 @@ struct ray_pre {
 // 7 v_pk_fma_f32 + 2 v_cmp; one scalar OR of the ballots decides whether any
 // lane needs the sqrt / interval work.  orig maps slots to original indices
 // (BVH order); nullptr = identity (brute-force order).
-template <bool OPEN, int NP, bool STATS>
+// The dot products take the y term first, h = fma(cz,dz, fma(cx,dx, fma(cy,dy, nk1)))
+// (DESIGN.md 2).  NOY: every sphere has the BVH layer's centre y, and r.nk1 /
+// r.o2 already hold fma(cy, dy, nk1) / fma(cy, -2 oy, o2) -- the same bits with
+// 5 instead of 7 v_pk_fma_f32 per pair.
+template <bool OPEN, int NP, bool STATS, bool NOY = false>
 __device__ __forceinline__ void scan_pairs(const RT_CONST pair_geom *__restrict__ g, int slot0,
                                            const RT_CONST int *__restrict__ orig, const ray_pre &r,
                                            hit_state &hs, uint32_t &roots) {
@@ -363,8 +367,10 @@ __device__ __forceinline__ void scan_pairs(const RT_CONST pair_geom *__restrict_
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
     q[j] = cload(g + j);
-    h[j] = fma2(q[j].cz, r.dz, fma2(q[j].cy, r.dy, fma2(q[j].cx, r.dx, r.nk1)));
-    const f2 gg = fma2(q[j].cz, r.oz2, fma2(q[j].cy, r.oy2, fma2(q[j].cx, r.ox2, r.o2)));
+    const f2 hy = NOY ? r.nk1 : fma2(q[j].cy, r.dy, r.nk1);
+    const f2 gy = NOY ? r.o2 : fma2(q[j].cy, r.oy2, r.o2);
+    h[j] = fma2(q[j].cz, r.dz, fma2(q[j].cx, r.dx, hy));
+    const f2 gg = fma2(q[j].cz, r.oz2, fma2(q[j].cx, r.ox2, gy));
     e[j] = fma2(h[j], h[j], -gg);
     // discriminant >= 0  <=>  e >= ks  (exact for finite floats)
     c[2 * j] = e[j].x >= q[j].ks.x;
@@ -457,10 +463,10 @@ __device__ __forceinline__ int walk_step(const bvh_node &nd, int node, bool hit,
   const int fp = (int)(nd.leaf & ~kTwoPairs) - 1;
   // a leaf of 1-2 spheres scans one pair, not a pair of padding
   if (nd.leaf & kTwoPairs) {
-    scan_pairs<OPEN, 2, STATS>(geom + fp, 2 * fp, orig, rp, hs, wc.roots);
+    scan_pairs<OPEN, 2, STATS, LAYER>(geom + fp, 2 * fp, orig, rp, hs, wc.roots);
     if (STATS) wc.tests += 4;
   } else {
-    scan_pairs<OPEN, 1, STATS>(geom + fp, 2 * fp, orig, rp, hs, wc.roots);
+    scan_pairs<OPEN, 1, STATS, LAYER>(geom + fp, 2 * fp, orig, rp, hs, wc.roots);
     if (STATS) wc.tests += 2;
   }
   if (LAYER) asm("v_min_f32 %0, %1, %2" : "=v"(lim) : "v"(lim_src), "v"(hs.tmax));
@@ -533,6 +539,10 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
       // a wave none of whose rays crosses the layer before tmax skips the walk
       int node = __builtin_amdgcn_ballot_w64(tyl_n <= tyl_fc) ? 0 : p.n_nodes;
       const f2 vi = {ix, iz}, vo = {oix, oiz}, va = {fabsf(ix), fabsf(iz)};
+      // leaves: the layer's shared centre y folded into the per-ray terms once
+      ray_pre rl = rp;
+      rl.nk1 = fma2(f2{p.layer_cy, p.layer_cy}, rp.dy, rp.nk1);
+      rl.o2 = fma2(f2{p.layer_cy, p.layer_cy}, rp.oy2, rp.o2);
       while (node < p.n_nodes) {
         const bvh_node nd = cload(order + node);
         // bz is unused here, but naming it keeps the node one s_load_dwordx8
@@ -547,7 +557,7 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
         float tn, tf;
         asm("v_max3_f32 %0, %1, %2, %3" : "=v"(tn) : "v"(tn2.x), "v"(tn2.y), "v"(tyl_n));
         asm("v_min3_f32 %0, %1, %2, %3" : "=v"(tf) : "v"(tf2.x), "v"(tf2.y), "v"(tyl_fc));
-        node = walk_step<OPEN, STATS, true>(nd, node, tn <= tf, geom, orig, rp, hs, wc, tyl_f, tyl_fc);
+        node = walk_step<OPEN, STATS, true>(nd, node, tn <= tf, geom, orig, rl, hs, wc, tyl_f, tyl_fc);
       }
     } else {
       const f2 vix = {ix, ix}, viy = {iy, iy}, viz = {iz, iz};
@@ -630,7 +640,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   if (alive) {
     int col, grow;
     pixel_cr(p, col, grow);
-    camera_ray(p, pix, col, grow, s_begin, ox, oy, oz, dx, dy, dz);
+    camera_ray(p, pcg4d(pix, s_begin, 0u, p.seed32), col, grow, ox, oy, oz, dx, dy, dz);
     sample = s_begin + 1;
   }
 
@@ -647,9 +657,15 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
       const float tmax = hs.tmax;
       const int best = hs.best;
       const bool near = hs.near;
+      // One hash per lane and step: a hit draws its bounce, pcg4d(pix, sample,
+      // depth + 1); a miss ends the path and draws the next sample's camera
+      // ray, pcg4d(pix, sample + 1, 0) (the same values as drawing each where
+      // it is used; only absorbed paths need a second hash below)
+      const bool miss = best < 0;
+      const uint4 r = pcg4d(pix, miss ? sample : sample - 1u, miss ? 0u : (uint32_t)(depth + 1), q.seed32);
 
       bool path_done = false;
-      if (best < 0) {
+      if (miss) {
         // miss: sky gradient, src/cpu/main.cc:27-29
         const float a = 0.5f * (dy + 1.0f);
         const float s0 = 1.0f - a;
@@ -671,7 +687,6 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           ny = -ny;
           nz = -nz;
         }
-        const uint4 r = pcg4d(pix, sample - 1u, (uint32_t)(depth + 1), q.seed32);
         // shared by the material branches (computed once: lanes of one wave
         // usually hit several materials, so the branches all execute)
         const float dn = dot3(dx, dy, dz, nx, ny, nz);
@@ -762,7 +777,9 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           const kparams k = kernargs();  // camera re-read
           int col, grow;
           pixel_cr(k, col, grow);
-          camera_ray(k, pix, col, grow, sample, ox, oy, oz, dx, dy, dz);
+          uint4 rc = r;
+          if (!miss) rc = pcg4d(pix, sample, 0u, k.seed32);  // absorbed or depth limit
+          camera_ray(k, rc, col, grow, ox, oy, oz, dx, dy, dz);
           ++sample;
           depth = 0;
           thr = thg = thb = 1.0f;
@@ -844,7 +861,7 @@ struct rt_context {
   uint32_t n_spheres = 0, n_pad = 0, n_nodes = 0, n_bvh_slots = 0;
   float oref2 = 0.0f;
   bool layer_mode = false;
-  float layer_lo = 0.0f, layer_hi = 0.0f;
+  float layer_lo = 0.0f, layer_hi = 0.0f, layer_cy = 0.0f;
   uint32_t extra_pair0 = 0, n_extra_pairs = 0;
   unsigned long long *d_counters = nullptr;
   float *d_frame = nullptr;
@@ -1136,14 +1153,15 @@ struct bvh_builder {
   }
   // Layer mode.  The final scene is a thin layer of small spheres (all at
   // y = 0.2 with r = 0.2) plus the ground and three big spheres.  If most
-  // spheres share one (centre y, radius) and at most kMaxExtra do not lie in
-  // that layer's y-range, the BVH is built over the layer spheres only (every
-  // box then has the layer's y-range, so the walk computes that slab interval
-  // once per ray) and the rest are scanned as plain pairs.  Reorders ord:
+  // spheres share one (centre y, radius) and at most kMaxExtra do not, the BVH
+  // is built over the layer spheres only (every box then has the layer's
+  // y-range, so the walk computes that slab interval once per ray, and the
+  // shared centre y folds into the per-ray terms of the leaf scan) and the
+  // rest are scanned as plain pairs.  Reorders ord:
   // layer spheres first; returns their count (n when not in layer mode).
   static constexpr uint32_t kMinLayer = 64, kMaxExtra = 16;
   bool layer_mode = false;
-  float layer_lo = 0.0f, layer_hi = 0.0f;
+  float layer_lo = 0.0f, layer_hi = 0.0f, layer_cy = 0.0f;
   uint32_t extra_pair0 = 0, n_extra_pairs = 0;
   uint32_t split_layer(const rt_scene_view *s) {
     const uint32_t n = s->n;
@@ -1170,9 +1188,10 @@ struct bvh_builder {
         y1 = std::max(y1, sb[i].hi[1]);
       }
     std::vector<uint32_t> in, out;
-    for (uint32_t i = 0; i < n; ++i) (sb[i].lo[1] >= y0 && sb[i].hi[1] <= y1 ? in : out).push_back(i);
+    for (uint32_t i = 0; i < n; ++i) (key[i] == key[best] ? in : out).push_back(i);
     if (out.size() > kMaxExtra) return n;
     layer_mode = true;
+    layer_cy = key[best].first;
     std::copy(in.begin(), in.end(), ord.begin());
     std::copy(out.begin(), out.end(), ord.begin() + in.size());
     return (uint32_t)in.size();
@@ -1364,6 +1383,7 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
   c->oref2 = (float)(0.99 * bb.oref * bb.oref);
   c->layer_mode = bb.layer_mode;
   c->layer_lo = bb.layer_lo;
+  c->layer_cy = bb.layer_cy;
   c->layer_hi = bb.layer_hi;
   c->extra_pair0 = bb.extra_pair0;
   c->n_extra_pairs = bb.n_extra_pairs;
@@ -1406,6 +1426,7 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
   kp.oref2 = c->oref2;
   kp.layer = rtk::f2{c->layer_lo, c->layer_hi};
   kp.layer_mode = c->layer_mode ? 1 : 0;
+  kp.layer_cy = c->layer_cy;
   kp.extra_pair0 = (int)c->extra_pair0;
   kp.n_extra_pairs = (int)c->n_extra_pairs;
   kp.seed32 = (uint32_t)prm->seed ^ ((uint32_t)(prm->seed >> 32) * 0x9E3779B9u);
