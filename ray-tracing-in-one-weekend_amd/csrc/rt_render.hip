@@ -43,11 +43,12 @@ constexpr int kTile = 8;           // 8x8 pixels per wave
 constexpr int kWavesPerBlock = 4;  // 256 threads
 constexpr int kBlock = 64 * kWavesPerBlock;
 constexpr int kSpherePad = 8;      // scan unroll granularity
-// auto rt_params.units: below kSplitTiles tiles (12 waves per wave slot of
-// the chip: 256 CUs x 4 SIMDs x 7) every chunk gets its own wave; above it a
-// wave traces all of its tile's samples.  Measured on the headline frame
-// (tools/rank_times.py): 1 GPU (129 600 tiles) 466 ms unsplit vs
-// 483 split; a 1/8 share (16 320 tiles) 151 ms unsplit vs 65 split.
+// auto rt_params.units: below kSplitTiles tiles (86 016: 10.5 waves per wave
+// slot of the chip at 256 CUs x 4 SIMDs x 8) every chunk gets its own wave;
+// above it a wave traces all of its tile's samples.  Measured on the headline
+// frame (tools/rank_times.py, tools/units_frame.py): 1 GPU
+// (129 600 tiles) 302 ms unsplit vs 310 / 314 with units 2 / 4; a 1/2 share
+// (64 800 tiles) 175 ms unsplit vs 158 split, a 1/8 share 103 vs 42.
 constexpr long long kSplitTiles = 12LL * 256 * 4 * 7;
 
 typedef float f2 __attribute__((ext_vector_type(2)));

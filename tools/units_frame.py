@@ -1,0 +1,41 @@
+#!/usr/bin/env python3
+"""Kernel time of the whole headline frame on one GPU for given rt_params.units
+values (scheduling only: the image is identical for every value).
+
+    python tools/units_frame.py [--units 1 2 4] [--w 3840 --h 2160 --spp 500]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ray-tracing-in-one-weekend_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--units", type=int, nargs="+", default=[1, 2, 4])
+    ap.add_argument("--w", type=int, default=3840)
+    ap.add_argument("--h", type=int, default=2160)
+    ap.add_argument("--spp", type=int, default=500)
+    a = ap.parse_args()
+    import rtow
+    ctx = rtow.Context(0)
+    ctx.upload(rtow.final_scene())
+    cam = rtow.camera_cpu(aspect=a.w / a.h)
+    ref = None
+    for u in a.units:
+        p = rtow.make_params(a.w, a.h, a.spp, seed=0, flags=rtow.RT_FLAG_ACCEL_BVH)
+        p.units = u
+        img, st = ctx.render(cam, p)
+        if ref is None:
+            ref = img
+        print(json.dumps({"units": u, "kernel_ms": round(st.kernel_ms, 3),
+                          "identical": bool(np.array_equal(ref, img))}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
