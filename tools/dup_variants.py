@@ -18,14 +18,15 @@ SRC = os.path.join(ROOT, "ray-tracing-in-one-weekend_amd", "csrc", "rt_render.hi
 
 EDITS = {
     # the ray-box slab test of every BVH node visit
-    "box": [("        node = walk_step<OPEN, STATS, true>(nd, node, tn <= tf, geom, orig, rp, hs, wc, tyl_f, tyl_fc);",
-             """        f2 vx2 = vix, vz2 = viz;
-        asm volatile("" : "+v"(vx2), "+v"(vz2));
-        const f2 ux2 = fma2(nd.bx, vx2, vox), uz2 = fma2(nd.bz, vz2, voz);
-        const float n2 = fmaxf(fmaxf(fminf(ux2.x, ux2.y), fminf(uz2.x, uz2.y)), tyl_n);
-        const float f2_ = fminf(fminf(fmaxf(ux2.x, ux2.y), fmaxf(uz2.x, uz2.y)), tyl_fc);
+    "box": [("        node = walk_step<OPEN, STATS, true>(nd, node, tn <= tf, geom, orig, rl, hs, wc, tyl_f, tyl_fc);",
+             """        f2 vi2 = vi, va2 = va;
+        asm volatile("" : "+v"(vi2), "+v"(va2));
+        const f2 m2 = fma2(nd.bx, vi2, vo);
+        const f2 tn22 = fma2(-nd.by, va2, m2), tf22 = fma2(nd.by, va2, m2);
+        const float n2 = fmaxf(fmaxf(tn22.x, tn22.y), tyl_n);
+        const float f2_ = fminf(fminf(tf22.x, tf22.y), tyl_fc);
         asm volatile("" :: "v"(n2), "v"(f2_));
-        node = walk_step<OPEN, STATS, true>(nd, node, tn <= tf, geom, orig, rp, hs, wc, tyl_f, tyl_fc);""")],
+        node = walk_step<OPEN, STATS, true>(nd, node, tn <= tf, geom, orig, rl, hs, wc, tyl_f, tyl_fc);""")],
     # the scan of the spheres off the layer (layer mode)
     "extras": [("      if (STATS) wc.tests += 2 * p.n_extra_pairs;",
                 """      if (STATS) wc.tests += 2 * p.n_extra_pairs;
@@ -33,8 +34,8 @@ EDITS = {
         hit_state h2{__builtin_huge_valf(), -1, 1};
         ray_pre r2 = rp;
         asm volatile("" : "+v"(r2.dx), "+v"(r2.nk1));
-        for (int k = 0; k < p.n_extra_pairs; ++k)
-          scan_pairs<OPEN, 1, STATS>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, r2, h2, wc.roots);
+        for (int k = 0; k < p.n_extra_pairs; k += 2)
+          scan_pairs<OPEN, 2, STATS>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, r2, h2, wc.roots);
         asm volatile("" :: "v"(h2.tmax), "v"(h2.best));
       }""")],
     # the correctly rounded sqrt of each candidate sphere
@@ -46,11 +47,11 @@ EDITS = {
     asm volatile("" :: "v"(sq2));
     const float t0 = h - sq, t1 = h + sq;""")],
     # the bounce's pcg4d
-    "pcg": [("        const uint4 r = pcg4d(pix, sample - 1u, (uint32_t)(depth + 1), p.seed32);",
-             """        const uint4 r = pcg4d(pix, sample - 1u, (uint32_t)(depth + 1), p.seed32);
-        uint32_t pq = pix;
-        asm volatile("" : "+v"(pq));
-        const uint4 r2 = pcg4d(pq, sample - 1u, (uint32_t)(depth + 1), p.seed32);
+    "pcg": [("      const uint4 r = pcg4d(pix, miss ? sample : sample - 1u, miss ? 0u : (uint32_t)(depth + 1), q.seed32);",
+             """      const uint4 r = pcg4d(pix, miss ? sample : sample - 1u, miss ? 0u : (uint32_t)(depth + 1), q.seed32);
+      uint32_t pq = pix;
+      asm volatile("" : "+v"(pq));
+      const uint4 r2 = pcg4d(pq, miss ? sample : sample - 1u, miss ? 0u : (uint32_t)(depth + 1), q.seed32);
         asm volatile("" :: "v"(r2.x), "v"(r2.y), "v"(r2.z));""")],
     # sin/cos of the bounce's unit vector
     "sincos": [("  sincos_turn(u2, s, c);\n  x = r * c;",
@@ -68,15 +69,16 @@ EDITS = {
         const float t2 = refine_root(sr, tq, near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2);
         asm volatile("" :: "v"(t2));""")],
     # the camera ray of the next sample (path regeneration)
-    "camera": [("          camera_ray(kernargs(), pix, col, grow, sample, ox, oy, oz, dx, dy, dz);  // camera re-read",
-                """          camera_ray(kernargs(), pix, col, grow, sample, ox, oy, oz, dx, dy, dz);  // camera re-read
+    "camera": [("          camera_ray(k, rc, col, grow, ox, oy, oz, dx, dy, dz);",
+                """          camera_ray(k, rc, col, grow, ox, oy, oz, dx, dy, dz);
           {
-            uint32_t sq = sample;
-            asm volatile("" : "+v"(sq));
+            uint4 r2 = rc;
+            asm volatile("" : "+v"(r2.x), "+v"(r2.y), "+v"(r2.z), "+v"(r2.w));
             float a0, a1, a2, a3, a4, a5;
-            camera_ray(kernargs(), pix, col, grow, sq, a0, a1, a2, a3, a4, a5);
+            camera_ray(k, r2, col, grow, a0, a1, a2, a3, a4, a5);
             asm volatile("" :: "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5));
           }""")],
+    # the material scatter (all three branches as the wave runs them)
 }
 
 
