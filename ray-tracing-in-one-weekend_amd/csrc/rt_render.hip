@@ -13,11 +13,15 @@
 //    as soon as a path ends ("path regeneration"), so every bounce iteration
 //    of the wave does useful work on every lane until that lane's pixel is
 //    finished; the wave exits on __ballot(alive) == 0;
-//  * the closest-hit scan walks the sphere array with a wave-uniform index:
-//    sphere data are scalar (SMEM) loads into SGPRs that feed the VALU
-//    directly -- 7 FMAs + 1 compare per ray-sphere test, no LDS traffic, no
-//    per-sphere divergence; the square root and the interval test run only
-//    in the (rare) branch where some lane's discriminant is non-negative;
+//  * closest hit: a wave-uniform, stackless BVH walk (in the
+//    final scene a tree over the thin layer of small spheres, 3.2) or the
+//    brute-force scan; node and sphere records are scalar (SMEM) loads into
+//    SGPRs that feed v_pk_fma_f32 directly -- no LDS traffic, no per-lane
+//    divergence; the square root and the interval test run only in the
+//    branch where some lane's discriminant is non-negative;
+//  * 8 waves per SIMD: kernel parameters are re-read from the kernarg segment
+//    where they are used and per-lane coordinates recomputed, so nothing
+//    rarely used stays in registers across the bounce loop;
 //  * counter-based RNG (pcg4d keyed by pixel, sample, bounce slot, seed):
 //    no per-pixel state, results independent of launch geometry and of the
 //    number of GPUs;
@@ -547,7 +551,7 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
       while (node < p.n_nodes) {
         const bvh_node nd = cload(order + node);
         // bz is unused here, but naming it keeps the node one s_load_dwordx8
-        // (else x2 + x4: 338 vs 342 ms)
+        // (else x2 + x4: measured 1 % slower)
         asm volatile("" ::"s"(nd.bz.x), "s"(nd.bz.y));
         const f2 m = fma2(nd.bx, vi, vo);
         const f2 tn2 = fma2(-nd.by, va, m);
