@@ -14,7 +14,12 @@
 //   --width N --height N --spp N --depth N --seed N --spheres K (grid half
 //   extent; 11 = reference, 50 = 10k spheres) --scene final|five
 //   --camera cpu|gpu --semantics cpu|gpu --accel bvh|scan --gpus N --device N
-//   --out FILE --p6 --quiet
+//   --gather rccl|host --out FILE --p6 --quiet
+// With --gpus N > 1 the frame is split into interleaved 8-row bands, one
+// context and stream per device, and the tiles are gathered to device 0 with
+// one RCCL ncclGather over xGMI (single process, ncclCommInitAll); device 0's
+// gathered frame is copied to the host once.  --gather host copies each tile
+// back instead (no RCCL); --gather rccl forces the RCCL path also on 1 GPU.
 #include <fcntl.h>
 #include <unistd.h>
 
@@ -27,6 +32,9 @@
 #include <string>
 #include <thread>
 #include <vector>
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include "rt.h"
 
@@ -42,6 +50,7 @@ struct options {
   unsigned flags = 0;
   bool bvh = true;  // BVH walk (bit-identical to the scan)
   int gpus = 1, device = 0;
+  std::string gather = "auto";  // auto: rccl when gpus > 1
   std::string out;
   bool p6 = false, quiet = false;
 };
@@ -60,7 +69,7 @@ void check(int st, const char *what) {
                "usage: %s [--width N] [--height N] [--spp N] [--depth N] [--seed N]\n"
                "          [--spheres HALF_EXTENT] [--scene final|five] [--camera cpu|gpu]\n"
                "          [--semantics cpu|gpu] [--accel bvh|scan] [--gpus N] [--device N]\n"
-               "          [--out FILE] [--p6] [--quiet]\n",
+               "          [--gather rccl|host] [--out FILE] [--p6] [--quiet]\n",
                argv0);
   std::exit(2);
 }
@@ -105,6 +114,7 @@ int main(int argc, char **argv) {
     else if (a == "--accel") o.bvh = std::string(next()) != "scan";
     else if (a == "--gpus") o.gpus = std::atoi(next());
     else if (a == "--device") o.device = std::atoi(next());
+    else if (a == "--gather") o.gather = next();
     else if (a == "--out") o.out = next();
     else if (a == "--p6") o.p6 = true;
     else if (a == "--quiet") o.quiet = true;
@@ -116,6 +126,7 @@ int main(int argc, char **argv) {
   }
   if (gpu_mode && !o.seed_set) o.seed = (unsigned long long)std::time(nullptr);  // main.cu:88
   if (o.width < 2 || o.height < 2 || o.spp < 0 || o.depth < 0 || o.gpus < 1) usage(argv[0]);
+  if (o.gather != "auto" && o.gather != "rccl" && o.gather != "host") usage(argv[0]);
 
   // ---- scene (random_scene / new_world) ----
   const uint32_t cap = (uint32_t)(4 * o.half_extent * o.half_extent + 16);
@@ -186,15 +197,76 @@ int main(int argc, char **argv) {
     check(rt_context_create(jobs[g].device, &ctxs[g]), "rt_context_create");
     check(rt_scene_upload(ctxs[g], &view), "rt_scene_upload");
   }
-  auto start = std::chrono::high_resolution_clock::now();
-  std::vector<std::thread> threads;
-  for (int g = 0; g < o.gpus; ++g)
-    threads.emplace_back([&, g]() {
-      jobs[g].status = rt_render(ctxs[g], &cam, &jobs[g].params, jobs[g].host.data(), &jobs[g].stats);
-    });
-  for (auto &t : threads) t.join();
-  auto end = std::chrono::high_resolution_clock::now();
-  for (int g = 0; g < o.gpus; ++g) check(jobs[g].status, "rt_render");
+  const bool use_rccl = o.gather == "rccl" || (o.gather == "auto" && o.gpus > 1);
+  std::vector<float> gathered;  // rccl: device 0's tiles, rank-major
+  std::chrono::high_resolution_clock::time_point start, end;
+  if (use_rccl) {
+    // every device renders its tile on its own stream (launches are
+    // asynchronous: one host thread), then one ncclGather to device 0
+    const size_t tile = 3 * (size_t)o.width * jobs[0].params.local_rows;
+    std::vector<int> devs(o.gpus);
+    for (int g = 0; g < o.gpus; ++g) devs[g] = jobs[g].device;
+    std::vector<ncclComm_t> comms(o.gpus);
+    // RCCL prints a version banner on stdout, which carries the PPM: send it
+    // to stderr while the communicators are created
+    std::fflush(stdout);
+    const int saved_stdout = ::dup(1);
+    ::dup2(2, 1);
+    const ncclResult_t init = ncclCommInitAll(comms.data(), o.gpus, devs.data());
+    std::fflush(stdout);
+    ::dup2(saved_stdout, 1);
+    ::close(saved_stdout);
+    if (init != ncclSuccess) die("ncclCommInitAll", RT_ERR_HIP);
+    std::vector<hipStream_t> streams(o.gpus);
+    std::vector<float *> d_tile(o.gpus, nullptr);
+    float *d_all = nullptr;
+    for (int g = 0; g < o.gpus; ++g) {
+      if (hipSetDevice(devs[g]) != hipSuccess || hipStreamCreateWithFlags(&streams[g], hipStreamNonBlocking) != hipSuccess ||
+          hipMalloc(&d_tile[g], tile * sizeof(float)) != hipSuccess)
+        die("device buffers", RT_ERR_HIP);
+      if (g == 0 && hipMalloc(&d_all, tile * o.gpus * sizeof(float)) != hipSuccess) die("gather buffer", RT_ERR_HIP);
+    }
+    for (int g = 0; g < o.gpus; ++g) {
+      (void)hipSetDevice(devs[g]);
+      (void)hipDeviceSynchronize();
+    }
+    start = std::chrono::high_resolution_clock::now();
+    for (int g = 0; g < o.gpus; ++g)
+      check(rt_render_async(ctxs[g], &cam, &jobs[g].params, d_tile[g], streams[g]), "rt_render_async");
+    if (ncclGroupStart() != ncclSuccess) die("ncclGroupStart", RT_ERR_HIP);
+    for (int g = 0; g < o.gpus; ++g)
+      if (ncclGather(d_tile[g], g == 0 ? d_all : nullptr, tile, ncclFloat32, 0, comms[g], streams[g]) != ncclSuccess)
+        die("ncclGather", RT_ERR_HIP);
+    if (ncclGroupEnd() != ncclSuccess) die("ncclGroupEnd", RT_ERR_HIP);
+    for (int g = 0; g < o.gpus; ++g) {
+      (void)hipSetDevice(devs[g]);
+      if (hipStreamSynchronize(streams[g]) != hipSuccess) die("render + gather", RT_ERR_HIP);
+    }
+    end = std::chrono::high_resolution_clock::now();
+    gathered.resize(tile * o.gpus);
+    (void)hipSetDevice(devs[0]);
+    if (hipMemcpy(gathered.data(), d_all, gathered.size() * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
+      die("gather copy", RT_ERR_HIP);
+    for (int g = 0; g < o.gpus; ++g) {
+      check(rt_collect_stats(ctxs[g], &jobs[g].stats), "rt_collect_stats");
+      (void)hipSetDevice(devs[g]);
+      (void)hipFree(d_tile[g]);
+      (void)hipStreamDestroy(streams[g]);
+      ncclCommDestroy(comms[g]);
+    }
+    (void)hipSetDevice(devs[0]);
+    (void)hipFree(d_all);
+  } else {
+    start = std::chrono::high_resolution_clock::now();
+    std::vector<std::thread> threads;
+    for (int g = 0; g < o.gpus; ++g)
+      threads.emplace_back([&, g]() {
+        jobs[g].status = rt_render(ctxs[g], &cam, &jobs[g].params, jobs[g].host.data(), &jobs[g].stats);
+      });
+    for (auto &t : threads) t.join();
+    end = std::chrono::high_resolution_clock::now();
+    for (int g = 0; g < o.gpus; ++g) check(jobs[g].status, "rt_render");
+  }
 
   // main.cu:134-139 timing lines
   float ms = std::chrono::duration<float, std::milli>(end - start).count();
@@ -216,12 +288,12 @@ int main(int argc, char **argv) {
   std::vector<float> frame(3 * (size_t)o.width * o.height, 0.0f);
   for (int g = 0; g < o.gpus; ++g) {
     const rt_params &p = jobs[g].params;
+    const float *src = use_rccl ? &gathered[3 * (size_t)o.width * p.local_rows * g] : jobs[g].host.data();
     for (int r = 0; r < p.local_rows; ++r) {
       const int band = r / p.row_block;
       const int grow = (band * p.band_stride + p.band_offset) * p.row_block + r % p.row_block;
       if (grow >= o.height) continue;
-      std::memcpy(&frame[3 * (size_t)grow * o.width], &jobs[g].host[3 * (size_t)r * o.width],
-                  3 * sizeof(float) * o.width);
+      std::memcpy(&frame[3 * (size_t)grow * o.width], &src[3 * (size_t)r * o.width], 3 * sizeof(float) * o.width);
     }
   }
   std::vector<uint8_t> rgb(frame.size());
