@@ -68,6 +68,8 @@ def parse():
                          "on a one-GPU box (tiles staged through host memory)")
     ap.add_argument("--cpu-spp", type=int, default=30, help="spp of the bounded CPU sample (400x225)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pilot", action="store_true",
+                    help="launch tiles in index order (no RT_FLAG_PILOT_SCHEDULE)")
     ap.add_argument("--out", default="", help="write the gathered frame as PPM (P6 if .pgm/.p6)")
     a = ap.parse_args()
     if a.preset:
@@ -146,6 +148,11 @@ def main():
     ctx.upload(scene)
     params = rtow_dist.partition(W, H, spp, world, rank, a.row_block, max_depth=a.depth)
     params.flags |= rtow.RT_FLAG_KEEP_COUNTERS
+    if not a.no_pilot:
+        # launch the expensive tiles first: the 4-spp pilot that measures them
+        # runs in the first (warmup) frame of this geometry; timed frames reuse
+        # the order (include/rt.h RT_FLAG_PILOT_SCHEDULE)
+        params.flags |= rtow.RT_FLAG_PILOT_SCHEDULE
     if a.accel == "bvh":
         params.flags |= rtow.RT_FLAG_ACCEL_BVH
     tile = torch.zeros((params.local_rows, W, 3), dtype=torch.float32, device=dev)
@@ -256,6 +263,8 @@ def main():
             "lane_efficiency": round(segments / (64.0 * wave_steps), 4) if wave_steps else None,
             "kernel_ms_avg_rank0": round(k_avg_s * 1e3, 3),
             "accel": a.accel,
+            "schedule": "launch order" if a.no_pilot else
+                        "pilot (expensive tiles first; 4-spp pilot in the warmup frame)",
             "work_per_launch_rank0": {"segments": work.segments, "sphere_tests": work.sphere_tests,
                                       "box_tests": work.box_tests, "box_hits_own_ray": work.box_hits,
                                       "brute_force_equiv_tests": work.bf_tests},

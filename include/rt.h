@@ -64,7 +64,12 @@ enum {
   RT_FLAG_ACCEL_BVH = 1u << 9,
   /* count executed ray-sphere and ray-box tests (rt_stats.sphere_tests /
    * box_tests); selects an instrumented kernel build, for measurement runs */
-  RT_FLAG_COUNT_WORK = 1u << 10
+  RT_FLAG_COUNT_WORK = 1u << 10,
+  /* scheduling, not semantics: launch the most expensive tiles first.  The
+   * first render of a new frame geometry (size, band, camera, flags) runs a
+   * 4-spp pilot that measures every tile's segments and synchronises the
+   * stream once to sort them; later renders reuse the order. */
+  RT_FLAG_PILOT_SCHEDULE = 1u << 11
 };
 
 /* Scene as structure-of-arrays; n spheres.  Replaces the device-heap

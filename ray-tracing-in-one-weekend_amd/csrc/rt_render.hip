@@ -35,6 +35,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <string>
 #include <vector>
 
 #include "rt.h"
@@ -54,6 +55,11 @@ constexpr int kSpherePad = 8;      // scan unroll granularity
 // (129 600 tiles) 302 ms unsplit vs 310 / 314 with units 2 / 4; a 1/2 share
 // (64 800 tiles) 175 ms unsplit vs 158 split, a 1/8 share 103 vs 42.
 constexpr long long kSplitTiles = 12LL * 256 * 4 * 7;
+// With the pilot schedule (RT_FLAG_PILOT_SCHEDULE) the expensive tiles start
+// first, so the tail is short without splitting down to 6 waves per slot: a
+// 1/2 share (64 800 tiles) 151 ms unsplit vs 154 split, a 1/4 share (32 400)
+// 87 unsplit vs 78 split, 1/8 40 ms split (tools/rank_times.py --pilot).
+constexpr long long kSplitTilesPilot = 6LL * 256 * 4 * 8;
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -118,6 +124,10 @@ struct kparams {
   float *out;
   float *chunks;
   unsigned long long *counters;
+  // block schedule (nullptr = launch order): block_order[blockIdx] is the
+  // block of work to run, most expensive first (rt_context tile-cost pilot)
+  const uint32_t *block_order;
+  uint32_t *tile_cost;  // pilot renders: segments traced per tile
 };
 
 // The kernel arguments, re-read from the kernarg segment (constant address
@@ -606,8 +616,9 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   // and the lane its global pixel index; column, row and the s_tot slot are
   // recomputed from lane_now() where they are used.
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x) >> 6;
-  const int unit = (int)(blockIdx.x % (unsigned)p.units);
-  const int tile = (int)(blockIdx.x / (unsigned)p.units) * kWavesPerBlock + wave;
+  const unsigned bid = p.block_order ? as_const(p.block_order)[blockIdx.x] : blockIdx.x;
+  const int unit = (int)(bid % (unsigned)p.units);
+  const int tile = (int)(bid / (unsigned)p.units) * kWavesPerBlock + wave;
   const int col0 = (tile % p.tiles_x) * kTile, lrow0 = (tile / p.tiles_x) * kTile;
   uint32_t pix;
   bool valid;
@@ -821,6 +832,10 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
     }
   }
   if (lane == 0) {
+    if (STATS) {  // pilot renders (units = 1, launch order): segments per tile
+      const kparams k = kernargs();
+      if (k.tile_cost) k.tile_cost[(int)blockIdx.x * kWavesPerBlock + wave] = s;
+    }
     unsigned long long *counters = kernargs().counters;  // (4 atomics per wave)
     atomicAdd(&counters[0], (unsigned long long)s);
     atomicAdd(&counters[1], (unsigned long long)steps);
@@ -872,6 +887,10 @@ struct rt_context {
   float *d_frame = nullptr;
   size_t frame_floats = 0;
   float *d_chunks = nullptr;  // chunk sums of units > 0 (RT_CHUNK_SPP), grown on demand
+  // block schedule from a pilot render, cached per frame geometry
+  uint32_t *d_order = nullptr;
+  size_t order_n = 0;
+  std::vector<uint64_t> order_key;
   size_t chunk_floats = 0;
   uint64_t last_samples = 0;
   bool last_stats = false;
@@ -1228,7 +1247,7 @@ void launch(unsigned blocks, hipStream_t st, const rtk::kparams &kp0, rt_context
   kp.shade = c->d_shade;
   kp.out = out;
   kp.chunks = chunks;
-  kp.counters = c->d_counters;
+  if (!kp.counters) kp.counters = c->d_counters;  // (the pilot brings its own)
   rtk::render_kernel<O, U, B, S><<<blocks, rtk::kBlock, 0, st>>>(kp);
 }
 
@@ -1322,6 +1341,7 @@ void rt_context_destroy(rt_context *c) {
   (void)hipFree(c->d_counters);
   (void)hipFree(c->d_frame);
   (void)hipFree(c->d_chunks);
+  (void)hipFree(c->d_order);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1463,7 +1483,8 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
   // time, so the chunks are split over `units` waves (tools/rank_times.py).
   const int n_chunks = std::max(1, (prm->spp + RT_CHUNK_SPP - 1) / RT_CHUNK_SPP);
   long long units = prm->units;
-  if (units <= 0) units = tiles < rtk::kSplitTiles ? n_chunks : 1;
+  if (units <= 0)
+    units = tiles < ((prm->flags & RT_FLAG_PILOT_SCHEDULE) ? rtk::kSplitTilesPilot : rtk::kSplitTiles) ? n_chunks : 1;
   if (prm->spp <= 0 || prm->max_depth <= 0) units = 1;  // nothing is traced
   units = std::max(1LL, std::min<long long>(units, n_chunks));
   const int cpu = (int)((n_chunks + units - 1) / units);
@@ -1484,6 +1505,56 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
       c->chunk_floats = need;
     }
     chunks = c->d_chunks;
+  }
+  if ((prm->flags & RT_FLAG_PILOT_SCHEDULE) && prm->spp > 0 && prm->max_depth > 0 && blocks > 1) {
+    // Expensive tiles first (RT_FLAG_PILOT_SCHEDULE): a 4-spp pilot (same
+    // geometry, one wave per tile, the instrumented build that reports each
+    // tile's segments) runs once per frame geometry; blocks are then launched
+    // in decreasing cost of their tiles (longest-processing-time first), the
+    // units of a tile group adjacent.  Without it the hardware launches
+    // blocks in index order and the last wave slots to fill may get the most
+    // expensive tiles.  Scheduling only: the image does not depend on it.
+    std::vector<uint64_t> key = {(uint64_t)prm->width, (uint64_t)prm->height, (uint64_t)prm->local_rows,
+                                 (uint64_t)prm->row_block, (uint64_t)prm->band_stride,
+                                 (uint64_t)prm->band_offset, (uint64_t)units, (uint64_t)(prm->flags & 0x2ffu)};
+    const uint32_t *cw = reinterpret_cast<const uint32_t *>(cam);
+    for (size_t k = 0; k < sizeof(rt_camera) / 4; ++k) key.push_back(cw[k]);
+    if (key != c->order_key || c->order_n != (size_t)blocks * units) {
+      // tile costs, then 8 scratch counters (the context's are not touched)
+      const size_t n_cost = (size_t)blocks * rtk::kWavesPerBlock;
+      const size_t cost_bytes = (n_cost * sizeof(uint32_t) + 7) / 8 * 8;
+      uint32_t *d_cost = nullptr;
+      RT_HIP(hipMalloc(&d_cost, cost_bytes + 8 * sizeof(unsigned long long)));
+      RT_HIP(hipMemsetAsync(d_cost, 0, cost_bytes + 8 * sizeof(unsigned long long), st));
+      rtk::kparams pk = kp;
+      pk.spp = std::min(prm->spp, 4);
+      pk.n_chunks = 1;
+      pk.units = 1;
+      pk.chunks_per_unit = 1;
+      pk.tile_cost = d_cost;
+      pk.counters = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(d_cost) + cost_bytes);
+      kLaunch[(v & 7) | 8](blocks, st, pk, c, accum_rgb, nullptr);
+      RT_HIP(hipGetLastError());
+      std::vector<uint32_t> cost((size_t)blocks * rtk::kWavesPerBlock);
+      RT_HIP(hipMemcpyAsync(cost.data(), d_cost, cost.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      RT_HIP(hipStreamSynchronize(st));
+      (void)hipFree(d_cost);
+      std::vector<uint64_t> bc(blocks, 0);
+      for (size_t t = 0; t < cost.size(); ++t) bc[t / rtk::kWavesPerBlock] += cost[t];
+      std::vector<uint32_t> tb(blocks);
+      for (uint32_t b = 0; b < blocks; ++b) tb[b] = b;
+      std::stable_sort(tb.begin(), tb.end(), [&](uint32_t a, uint32_t b) { return bc[a] > bc[b]; });
+      std::vector<uint32_t> order((size_t)blocks * units);
+      for (size_t i = 0; i < tb.size(); ++i)
+        for (long long u = 0; u < units; ++u) order[i * units + u] = (uint32_t)(tb[i] * units + u);
+      (void)hipFree(c->d_order);
+      c->d_order = nullptr;
+      RT_HIP(hipMalloc(&c->d_order, order.size() * sizeof(uint32_t)));
+      RT_HIP(hipMemcpy(c->d_order, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+      c->order_n = order.size();
+      c->order_key = key;
+    }
+    kp.block_order = c->d_order;
   }
   kLaunch[v]((unsigned)(blocks * units), st, kp, c, accum_rgb, chunks);
   RT_HIP(hipGetLastError());

@@ -243,6 +243,34 @@ def test_units_do_not_change_the_image(rtow, gpu_ctx):
     assert np.array_equal(got, ref)
 
 
+def test_pilot_schedule_does_not_change_the_image(rtow, gpu_ctx):
+    """RT_FLAG_PILOT_SCHEDULE only reorders block launches (a 4-spp pilot per
+    frame geometry, then expensive tiles first): the same sums and segment
+    counts as launch order, for one wave per tile and for split chunks, on the
+    first render of a geometry (pilot + sort) and on a cached one; the pilot
+    leaves the context's counters alone (RT_FLAG_KEEP_COUNTERS)."""
+    gpu_ctx.upload(rtow.final_scene())
+    cam = rtow.camera_cpu(aspect=320 / 120)
+    bvh = rtow.RT_FLAG_ACCEL_BVH
+    pilot = bvh | rtow.RT_FLAG_PILOT_SCHEDULE
+    for units in (1, 3, 0):
+        ref, st = gpu_ctx.render(cam, rtow.make_params(320, 120, 200, seed=9, flags=bvh, units=units))
+        for _ in range(2):
+            got, st2 = gpu_ctx.render(cam, rtow.make_params(320, 120, 200, seed=9, flags=pilot, units=units))
+            assert np.array_equal(got, ref), units
+            assert st2.segments == st.segments
+    # a new geometry (another camera) gets its own pilot; counters accumulate
+    # only the real renders
+    cam2 = rtow.camera_cpu(aspect=320 / 120, lookfrom=(12.0, 2.5, 3.5))
+    a, sa = gpu_ctx.render(cam2, rtow.make_params(320, 120, 64, seed=2, flags=bvh))
+    gpu_ctx.reset_stats()
+    p = rtow.make_params(320, 120, 64, seed=2, flags=pilot | rtow.RT_FLAG_KEEP_COUNTERS)
+    b, _ = gpu_ctx.render(cam2, p)
+    c, _ = gpu_ctx.render(cam2, p)
+    assert np.array_equal(a, b) and np.array_equal(a, c)
+    assert gpu_ctx.collect_stats().segments == 2 * sa.segments
+
+
 def test_cli_bvh_and_scan_print_the_same_ppm(tmp_path):
     """bin/cpu_ray_tracer (the drop-in executable): P3 on stdout, identical bytes
     for --accel bvh (default) and --accel scan, and P6 with the same pixels."""

@@ -22,13 +22,18 @@ def main():
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--units", type=int, nargs="+", default=[0], help="rt_params.units values (0 = auto)")
+    ap.add_argument("--pilot", action="store_true",
+                    help="RT_FLAG_PILOT_SCHEDULE; every share is rendered twice and the second "
+                         "(with the cached tile order) is timed")
     a = ap.parse_args()
     import rtow
     ctx = rtow.Context(0)
     ctx.upload(rtow.final_scene())
     cam = rtow.camera_cpu(aspect=a.w / a.h)
-    flags = rtow.RT_FLAG_ACCEL_BVH
-    _, st = ctx.render(cam, rtow.make_params(a.w, a.h, a.spp, seed=0, flags=flags))
+    flags = rtow.RT_FLAG_ACCEL_BVH | (rtow.RT_FLAG_PILOT_SCHEDULE if a.pilot else 0)
+    reps = 2 if a.pilot else 1
+    for _ in range(reps):
+        _, st = ctx.render(cam, rtow.make_params(a.w, a.h, a.spp, seed=0, flags=flags))
     full = st.kernel_ms
     print(json.dumps({"world": 1, "kernel_ms": round(full, 2)}), flush=True)
     for g in a.world:
@@ -37,7 +42,8 @@ def main():
             for r in range(g):
                 p = rtow.make_params(a.w, a.h, a.spp, seed=0, flags=flags, rank=r, world=g,
                                      row_block=a.row_block, units=u)
-                _, st = ctx.render(cam, p)
+                for _ in range(reps):
+                    _, st = ctx.render(cam, p)
                 ms.append(st.kernel_ms)
             print(json.dumps({"world": g, "units": u, "rank_ms": [round(x, 2) for x in ms],
                               "max_ms": round(max(ms), 2), "ideal_ms": round(full / g, 2),
