@@ -175,8 +175,10 @@ int main(int argc, char **argv) {
     p.spp = o.spp;
     p.max_depth = o.depth;
     p.seed = o.seed;
-    // expensive tiles first (a 4-spp pilot, ~1 % of the frame, then ~4 % faster)
-    p.flags = o.flags | (o.bvh ? RT_FLAG_ACCEL_BVH : 0u) | RT_FLAG_PILOT_SCHEDULE;
+    // (no RT_FLAG_PILOT_SCHEDULE: the pilot pays off over repeated frames of
+    // one geometry, not in a one-frame process -- its first launch also loads
+    // the instrumented kernel)
+    p.flags = o.flags | (o.bvh ? RT_FLAG_ACCEL_BVH : 0u);
     if (o.gpus == 1) {
       p.row_block = o.height;
       p.band_stride = 1;
