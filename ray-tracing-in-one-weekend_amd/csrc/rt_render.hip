@@ -1277,6 +1277,7 @@ void free_scene(rt_context *c) {
   c->n_spheres = c->n_pad = c->n_nodes = c->n_bvh_slots = 0;
   c->layer_mode = false;
   c->extra_pair0 = c->n_extra_pairs = 0;
+  c->order_key.clear();  // the pilot's tile costs belong to the old scene
 }
 
 template <class T>
