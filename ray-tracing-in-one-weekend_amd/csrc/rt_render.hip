@@ -62,6 +62,12 @@ constexpr long long kSplitTiles = 12LL * 256 * 4 * 7;
 constexpr long long kSplitTilesPilot = 6LL * 256 * 4 * 8;
 
 typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// layer grid walk instead of the layer BVH walk (experiment switch)
+#ifndef RT_GRID
+#define RT_GRID 0
+#endif
 
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
@@ -128,6 +134,13 @@ struct kparams {
   // block of work to run, most expensive first (rt_context tile-cost pilot)
   const uint32_t *block_order;
   uint32_t *tile_cost;  // pilot renders: segments traced per tile
+  // layer grid (layer mode, bvh_builder::build_grid): x-z cells over the
+  // layer spheres; cell = (first item << 4) | item count, row-major [nz][nx];
+  // item = (cx, cz, ks, original index bits).  nullptr: walk the layer BVH.
+  const uint32_t *grid_cells;
+  const f4 *grid_items;
+  float grid_x0, grid_z0, grid_x1, grid_z1, grid_g, grid_invg;
+  int grid_nx, grid_nz;
 };
 
 // The kernel arguments, re-read from the kernarg segment (constant address
@@ -488,6 +501,58 @@ __device__ __forceinline__ int walk_step(const bvh_node &nd, int node, bool hit,
   return nd.skip;
 }
 
+// Per-lane 2-D DDA over the layer grid (layer mode): the lane visits the x-z
+// cells its own segment crosses inside the layer's y-slab, [ta, tb] clipped to
+// the grid box, in order, and tests the spheres listed in each cell with the
+// leaf test's arithmetic (NOY fold: same bits as scan_pairs).  It stops once
+// the next cell starts beyond min(tb, tmax).  Cell lists hold every sphere
+// whose padded box (the BVH's reach) comes within kGridPad of the cell, so
+// the fp32 DDA's boundary errors cannot skip a sphere the walk would test.
+template <bool OPEN, bool STATS>
+__device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz, float ta, float tb,
+                                          const ray_pre &rl, hit_state &hs, work_ctr &wc) {
+  const kparams p = kernargs();
+  const float ax = (p.grid_x0 - ox) * ix, bx = (p.grid_x1 - ox) * ix;
+  const float az = (p.grid_z0 - oz) * iz, bz = (p.grid_z1 - oz) * iz;
+  ta = fmaxf(ta, fmaxf(fminf(ax, bx), fminf(az, bz)));
+  tb = fminf(tb, fminf(fmaxf(ax, bx), fmaxf(az, bz)));
+  if (!(ta <= tb)) return;
+  const float dx = rl.dx.x, dz = rl.dz.x;
+  const float px = fmaf(ta, dx, ox), pz = fmaf(ta, dz, oz);
+  int cx = min(max((int)floorf((px - p.grid_x0) * p.grid_invg), 0), p.grid_nx - 1);
+  int cz = min(max((int)floorf((pz - p.grid_z0) * p.grid_invg), 0), p.grid_nz - 1);
+  const int sx = dx < 0.0f ? -1 : 1, sz = dz < 0.0f ? -1 : 1;
+  float tmx = (fmaf((float)(cx + (dx < 0.0f ? 0 : 1)), p.grid_g, p.grid_x0) - ox) * ix;
+  float tmz = (fmaf((float)(cz + (dz < 0.0f ? 0 : 1)), p.grid_g, p.grid_z0) - oz) * iz;
+  const float tdx = p.grid_g * fabsf(ix), tdz = p.grid_g * fabsf(iz);
+  const RT_GLOBAL uint32_t *__restrict__ cells = as_global(p.grid_cells);
+  const RT_GLOBAL f4 *__restrict__ items = as_global(p.grid_items);
+  const int nx = p.grid_nx, nz = p.grid_nz;
+  while (true) {
+    const uint32_t ce = cells[cz * nx + cx];
+    const uint32_t first = ce >> 4, cnt = ce & 15u;
+    if (STATS) ++wc.boxes;
+    for (uint32_t k = 0; k < cnt; ++k) {
+      const f4 it = items[first + k];
+      const float h = fmaf(it.y, dz, fmaf(it.x, dx, rl.nk1.x));
+      const float g = fmaf(it.y, rl.oz2.x, fmaf(it.x, rl.ox2.x, rl.o2.x));
+      const float e = fmaf(h, h, -g);
+      candidate<OPEN>(e >= it.z, h, e - it.z, __float_as_int(it.w), hs);
+      if (STATS) ++wc.tests;
+    }
+    if (fminf(tmx, tmz) > fminf(tb, hs.tmax)) break;
+    if (tmx < tmz) {
+      cx += sx;
+      tmx += tdx;
+      if ((unsigned)cx >= (unsigned)nx) break;
+    } else {
+      cz += sz;
+      tmz += tdz;
+      if ((unsigned)cz >= (unsigned)nz) break;
+    }
+  }
+}
+
 // Closest hit of the ray (o, d) over all spheres: hittable_list::hit,
 // src/cpu/hittable_list.h:28-43.  Wave-uniform: every active lane of the wave
 // calls it together; the result does not depend on which lanes those are.
@@ -551,6 +616,15 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
       const float tyl_n = fmaxf(fminf(tyl.x, tyl.y), 0.0f);
       const float tyl_f = fmaxf(tyl.x, tyl.y);
       float tyl_fc = fminf(tyl_f, hs.tmax);  // refreshed by walk_step after every leaf
+#if RT_GRID
+      if (p.grid_cells) {
+        ray_pre rg = rp;
+        rg.nk1 = fma2(f2{p.layer_cy, p.layer_cy}, rp.dy, rp.nk1);
+        rg.o2 = fma2(f2{p.layer_cy, p.layer_cy}, rp.oy2, rp.o2);
+        if (tyl_n <= tyl_fc) grid_walk<OPEN, STATS>(ox, oz, ix, iz, tyl_n, tyl_fc, rg, hs, wc);
+        return hs;
+      }
+#endif
       // a wave none of whose rays crosses the layer before tmax skips the walk
       int node = __builtin_amdgcn_ballot_w64(tyl_n <= tyl_fc) ? 0 : p.n_nodes;
       const f2 vi = {ix, iz}, vo = {oix, oiz}, va = {fabsf(ix), fabsf(iz)};
@@ -883,6 +957,10 @@ struct rt_context {
   bool layer_mode = false;
   float layer_lo = 0.0f, layer_hi = 0.0f, layer_cy = 0.0f;
   uint32_t extra_pair0 = 0, n_extra_pairs = 0;
+  uint32_t *d_grid_cells = nullptr;  // layer grid (nullptr: none)
+  float *d_grid_items = nullptr;
+  float grid_x0 = 0, grid_z0 = 0, grid_x1 = 0, grid_z1 = 0, grid_g = 0;
+  int grid_nx = 0, grid_nz = 0;
   unsigned long long *d_counters = nullptr;
   float *d_frame = nullptr;
   size_t frame_floats = 0;
@@ -1173,6 +1251,81 @@ struct bvh_builder {
       // time (one s_load_dwordx16, two independent chains)
       while ((slots.size() - 2 * extra_pair0) % 4) slots.push_back(-1);
       n_extra_pairs = (uint32_t)slots.size() / 2 - extra_pair0;
+      if (RT_GRID) build_grid(s, n_tree);
+    }
+  }
+  // Layer grid: square x-z cells of side g over the layer spheres' padded
+  // boxes; a cell lists every layer sphere whose padded box comes within pad
+  // of it.  g is chosen for ~1 sphere per cell (RTOW_GRID_SCALE scales it);
+  // cells list at most 15 spheres (else g shrinks).
+  std::vector<uint32_t> grid_cells;
+  std::vector<float> grid_items;  // 4 floats per item
+  float grid_x0 = 0, grid_z0 = 0, grid_x1 = 0, grid_z1 = 0, grid_g = 0;
+  int grid_nx = 0, grid_nz = 0;
+  void build_grid(const rt_scene_view *s, uint32_t n_tree) {
+    double x0 = 1e300, x1 = -1e300, z0 = 1e300, z1 = -1e300;
+    for (uint32_t k = 0; k < n_tree; ++k) {
+      const uint32_t i = ord[k];
+      x0 = std::min(x0, sb[i].lo[0]);
+      x1 = std::max(x1, sb[i].hi[0]);
+      z0 = std::min(z0, sb[i].lo[2]);
+      z1 = std::max(z1, sb[i].hi[2]);
+    }
+    const double pad = 0x1p-10 * std::max(1.0, std::max(x1 - x0, z1 - z0) / 32.0);
+    x0 -= 2 * pad;
+    z0 -= 2 * pad;
+    x1 += 2 * pad;
+    z1 += 2 * pad;
+    double scale = 1.0;
+    if (const char *e = getenv("RTOW_GRID_SCALE")) scale = atof(e);
+    double g = scale * std::sqrt((x1 - x0) * (z1 - z0) / (double)n_tree);
+    for (int attempt = 0; attempt < 8; ++attempt, g *= 0.8) {
+      const int nx = (int)std::ceil((x1 - x0) / g), nz = (int)std::ceil((z1 - z0) / g);
+      if ((long long)nx * nz > (1 << 20)) return;
+      std::vector<std::vector<uint32_t>> lists((size_t)nx * nz);
+      bool ok = true;
+      for (uint32_t k = 0; k < n_tree && ok; ++k) {
+        const uint32_t i = ord[k];
+        const int a0 = std::max(0, (int)std::floor((sb[i].lo[0] - pad - x0) / g));
+        const int a1 = std::min(nx - 1, (int)std::floor((sb[i].hi[0] + pad - x0) / g));
+        const int b0 = std::max(0, (int)std::floor((sb[i].lo[2] - pad - z0) / g));
+        const int b1 = std::min(nz - 1, (int)std::floor((sb[i].hi[2] + pad - z0) / g));
+        for (int b = b0; b <= b1; ++b)
+          for (int a = a0; a <= a1; ++a) {
+            std::vector<uint32_t> &l = lists[(size_t)b * nx + a];
+            l.push_back(i);
+            if (l.size() > 15) ok = false;
+          }
+      }
+      if (!ok) continue;
+      grid_cells.assign((size_t)nx * nz, 0);
+      grid_items.clear();
+      for (size_t c = 0; c < lists.size(); ++c) {
+        grid_cells[c] = (uint32_t)(grid_items.size() / 4) << 4 | (uint32_t)lists[c].size();
+        for (uint32_t i : lists[c]) {
+          const double x = s->cx[i], y = s->cy[i], z = s->cz[i], r = s->radius[i];
+          grid_items.push_back(s->cx[i]);
+          grid_items.push_back(s->cz[i]);
+          grid_items.push_back((float)(x * x + y * y + z * z - r * r));
+          int32_t idx = (int32_t)i;
+          float f;
+          std::memcpy(&f, &idx, 4);
+          grid_items.push_back(f);
+        }
+      }
+      if (grid_items.size() / 4 >= (1u << 27)) {
+        grid_cells.clear();
+        grid_items.clear();
+        return;
+      }
+      grid_x0 = (float)x0;
+      grid_z0 = (float)z0;
+      grid_g = (float)g;
+      grid_nx = nx;
+      grid_nz = nz;
+      grid_x1 = (float)(x0 + nx * g);
+      grid_z1 = (float)(z0 + nz * g);
+      return;
     }
   }
   // Layer mode.  The final scene is a thin layer of small spheres (all at
@@ -1270,6 +1423,11 @@ void free_scene(rt_context *c) {
   (void)hipFree(c->d_nodes);
   (void)hipFree(c->d_orig);
   (void)hipFree(c->d_shade);
+  (void)hipFree(c->d_grid_cells);
+  (void)hipFree(c->d_grid_items);
+  c->d_grid_cells = nullptr;
+  c->d_grid_items = nullptr;
+  c->grid_nx = c->grid_nz = 0;
   c->d_geom = c->d_bvh_geom = nullptr;
   c->d_nodes = nullptr;
   c->d_orig = nullptr;
@@ -1397,6 +1555,10 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
   if (e == hipSuccess) e = upload_vec(&c->d_nodes, bb.nodes, c->stream);
   if (e == hipSuccess) e = upload_vec(&c->d_orig, bb.slots, c->stream);
   if (e == hipSuccess) e = upload_vec(&c->d_shade, shade, c->stream);
+  if (e == hipSuccess && !bb.grid_cells.empty()) {
+    e = upload_vec(&c->d_grid_cells, bb.grid_cells, c->stream);
+    if (e == hipSuccess) e = upload_vec(&c->d_grid_items, bb.grid_items, c->stream);
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
     free_scene(c);
@@ -1413,6 +1575,13 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
   c->layer_hi = bb.layer_hi;
   c->extra_pair0 = bb.extra_pair0;
   c->n_extra_pairs = bb.n_extra_pairs;
+  c->grid_x0 = bb.grid_x0;
+  c->grid_z0 = bb.grid_z0;
+  c->grid_x1 = bb.grid_x1;
+  c->grid_z1 = bb.grid_z1;
+  c->grid_g = bb.grid_g;
+  c->grid_nx = bb.grid_nx;
+  c->grid_nz = bb.grid_nz;
   return RT_OK;
 }
 
@@ -1455,6 +1624,16 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
   kp.layer_cy = c->layer_cy;
   kp.extra_pair0 = (int)c->extra_pair0;
   kp.n_extra_pairs = (int)c->n_extra_pairs;
+  kp.grid_cells = c->d_grid_cells;
+  kp.grid_items = (const rtk::f4 *)c->d_grid_items;
+  kp.grid_x0 = c->grid_x0;
+  kp.grid_z0 = c->grid_z0;
+  kp.grid_x1 = c->grid_x1;
+  kp.grid_z1 = c->grid_z1;
+  kp.grid_g = c->grid_g;
+  kp.grid_invg = c->grid_g > 0.0f ? 1.0f / c->grid_g : 0.0f;
+  kp.grid_nx = c->grid_nx;
+  kp.grid_nz = c->grid_nz;
   kp.seed32 = (uint32_t)prm->seed ^ ((uint32_t)(prm->seed >> 32) * 0x9E3779B9u);
   kp.flags = prm->flags;
   kp.inv_wm1 = (float)(1.0 / (prm->width - 1));
