@@ -69,7 +69,12 @@ enum {
    * first render of a new frame geometry (size, band, camera, flags) runs a
    * 4-spp pilot that measures every tile's segments and synchronises the
    * stream once to sort them; later renders reuse the order. */
-  RT_FLAG_PILOT_SCHEDULE = 1u << 11
+  RT_FLAG_PILOT_SCHEDULE = 1u << 11,
+  /* acceleration, not semantics (with RT_FLAG_ACCEL_BVH): when the scene is a
+   * thin layer of like spheres plus a few others, rt_scene_upload builds an
+   * x-z grid over the layer and the render walks it per lane;
+   * this flag walks the layer BVH instead.  Same image either way. */
+  RT_FLAG_LAYER_BVH = 1u << 12
 };
 
 /* Scene as structure-of-arrays; n spheres.  Replaces the device-heap

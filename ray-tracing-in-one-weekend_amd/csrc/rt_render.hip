@@ -64,11 +64,6 @@ constexpr long long kSplitTilesPilot = 6LL * 256 * 4 * 8;
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-// layer grid walk instead of the layer BVH walk (experiment switch)
-#ifndef RT_GRID
-#define RT_GRID 0
-#endif
-
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 // scan record for two consecutive spheres i, i+1 (32 B): every field is a
@@ -559,7 +554,7 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
 // The scene parameters are re-read from the kernarg segment on entry
 // (kernargs()): they live in SGPRs for the walk only, not across the whole
 // bounce loop (SGPR pressure).
-template <bool OPEN, bool BVH, bool STATS>
+template <bool OPEN, bool BVH, bool STATS, bool GRID>
 __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, float dx, float dy, float dz,
                                                  work_ctr &wc) {
   const kparams p = kernargs();
@@ -616,15 +611,13 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
       const float tyl_n = fmaxf(fminf(tyl.x, tyl.y), 0.0f);
       const float tyl_f = fmaxf(tyl.x, tyl.y);
       float tyl_fc = fminf(tyl_f, hs.tmax);  // refreshed by walk_step after every leaf
-#if RT_GRID
-      if (p.grid_cells) {
+      if (GRID) {  // the layer grid (its own kernel build: no BVH walk code)
         ray_pre rg = rp;
         rg.nk1 = fma2(f2{p.layer_cy, p.layer_cy}, rp.dy, rp.nk1);
         rg.o2 = fma2(f2{p.layer_cy, p.layer_cy}, rp.oy2, rp.o2);
         if (tyl_n <= tyl_fc) grid_walk<OPEN, STATS>(ox, oz, ix, iz, tyl_n, tyl_fc, rg, hs, wc);
         return hs;
       }
-#endif
       // a wave none of whose rays crosses the layer before tmax skips the walk
       int node = __builtin_amdgcn_ballot_w64(tyl_n <= tyl_fc) ? 0 : p.n_nodes;
       const f2 vi = {ix, iz}, vo = {oix, oiz}, va = {fabsf(ix), fabsf(iz)};
@@ -683,7 +676,7 @@ __device__ __forceinline__ int lane_now() {
 // the kernarg segment where they are used (kernargs(), as_const()) instead of
 // being held in SGPRs for the whole kernel: 94 SGPRs + 21 spilled -> 69 at 7
 // waves.
-template <bool OPEN, bool METAL_UNIT, bool BVH, bool STATS>
+template <bool OPEN, bool METAL_UNIT, bool BVH, bool STATS, bool GRID>
 __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   // Per-lane values that the bounce loop rarely needs are not kept live (VGPR
   // pressure at 8 waves): the wave keeps its tile origin (col0, lrow0, SGPRs)
@@ -737,7 +730,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   while (true) {
     hit_state hs{__builtin_huge_valf(), -1, 1};
     if (!__ballot(alive)) break;
-    if (alive) hs = closest_hit<OPEN, BVH, STATS>(ox, oy, oz, dx, dy, dz, wc);
+    if (alive) hs = closest_hit<OPEN, BVH, STATS, GRID>(ox, oy, oz, dx, dy, dz, wc);
     ++steps;
     if (alive) {
       ++segs;
@@ -1251,7 +1244,7 @@ struct bvh_builder {
       // time (one s_load_dwordx16, two independent chains)
       while ((slots.size() - 2 * extra_pair0) % 4) slots.push_back(-1);
       n_extra_pairs = (uint32_t)slots.size() / 2 - extra_pair0;
-      if (RT_GRID) build_grid(s, n_tree);
+      build_grid(s, n_tree);
     }
   }
   // Layer grid: square x-z cells of side g over the layer spheres' padded
@@ -1390,7 +1383,7 @@ void fill_slot(rtk::pair_geom &g, int l, const rt_scene_view *s, int i) {
   }
 }
 
-template <bool O, bool U, bool B, bool S>
+template <bool O, bool U, bool B, bool S, bool G = false>
 void launch(unsigned blocks, hipStream_t st, const rtk::kparams &kp0, rt_context *c, float *out, float *chunks) {
   rtk::kparams kp = kp0;
   kp.scan_geom = c->d_geom;
@@ -1401,12 +1394,13 @@ void launch(unsigned blocks, hipStream_t st, const rtk::kparams &kp0, rt_context
   kp.out = out;
   kp.chunks = chunks;
   if (!kp.counters) kp.counters = c->d_counters;  // (the pilot brings its own)
-  rtk::render_kernel<O, U, B, S><<<blocks, rtk::kBlock, 0, st>>>(kp);
+  rtk::render_kernel<O, U, B, S, G><<<blocks, rtk::kBlock, 0, st>>>(kp);
 }
 
 using launch_fn = void (*)(unsigned, hipStream_t, const rtk::kparams &, rt_context *, float *, float *);
-// index: open | unit<<1 | bvh<<2 | stats<<3
-const launch_fn kLaunch[16] = {
+// index: open | unit<<1 | bvh<<2 | stats<<3 | grid<<4 (grid: the layer grid
+// walk, a build of its own; without bvh the grid bit selects the scan)
+const launch_fn kLaunch[32] = {
     launch<false, false, false, false>, launch<true, false, false, false>,
     launch<false, true, false, false>,  launch<true, true, false, false>,
     launch<false, false, true, false>,  launch<true, false, true, false>,
@@ -1415,6 +1409,14 @@ const launch_fn kLaunch[16] = {
     launch<false, true, false, true>,   launch<true, true, false, true>,
     launch<false, false, true, true>,   launch<true, false, true, true>,
     launch<false, true, true, true>,    launch<true, true, true, true>,
+    launch<false, false, false, false>, launch<true, false, false, false>,
+    launch<false, true, false, false>,  launch<true, true, false, false>,
+    launch<false, false, true, false, true>,  launch<true, false, true, false, true>,
+    launch<false, true, true, false, true>,   launch<true, true, true, false, true>,
+    launch<false, false, false, true>,  launch<true, false, false, true>,
+    launch<false, true, false, true>,   launch<true, true, false, true>,
+    launch<false, false, true, true, true>,   launch<true, false, true, true, true>,
+    launch<false, true, true, true, true>,    launch<true, true, true, true, true>,
 };
 
 void free_scene(rt_context *c) {
@@ -1655,7 +1657,8 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
   const int v = ((prm->flags & RT_FLAG_OPEN_INTERVAL) ? 1 : 0) |
                 ((prm->flags & RT_FLAG_METAL_UNIT_VECTOR) ? 2 : 0) |
                 ((prm->flags & RT_FLAG_ACCEL_BVH) ? 4 : 0) |
-                ((prm->flags & RT_FLAG_COUNT_WORK) ? 8 : 0);
+                ((prm->flags & RT_FLAG_COUNT_WORK) ? 8 : 0) |
+                ((c->d_grid_cells && !(prm->flags & RT_FLAG_LAYER_BVH)) ? 16 : 0);
   // sample chunks (RT_CHUNK_SPP) and how many waves share a tile's chunks.
   // One wave per tile traces all of a pixel's samples in sequence; when a
   // rank holds few tiles (a 1/8 share of a 4K frame is ~2.3 waves per wave
@@ -1696,7 +1699,7 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
     // expensive tiles.  Scheduling only: the image does not depend on it.
     std::vector<uint64_t> key = {(uint64_t)prm->width, (uint64_t)prm->height, (uint64_t)prm->local_rows,
                                  (uint64_t)prm->row_block, (uint64_t)prm->band_stride,
-                                 (uint64_t)prm->band_offset, (uint64_t)units, (uint64_t)(prm->flags & 0x2ffu)};
+                                 (uint64_t)prm->band_offset, (uint64_t)units, (uint64_t)(prm->flags & 0x12ffu)};
     const uint32_t *cw = reinterpret_cast<const uint32_t *>(cam);
     for (size_t k = 0; k < sizeof(rt_camera) / 4; ++k) key.push_back(cw[k]);
     if (key != c->order_key || c->order_n != (size_t)blocks * units) {
@@ -1713,7 +1716,7 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
       pk.chunks_per_unit = 1;
       pk.tile_cost = d_cost;
       pk.counters = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(d_cost) + cost_bytes);
-      kLaunch[(v & 7) | 8](blocks, st, pk, c, accum_rgb, nullptr);
+      kLaunch[(v & 23) | 8](blocks, st, pk, c, accum_rgb, nullptr);
       RT_HIP(hipGetLastError());
       std::vector<uint32_t> cost((size_t)blocks * rtk::kWavesPerBlock);
       RT_HIP(hipMemcpyAsync(cost.data(), d_cost, cost.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));

@@ -32,6 +32,7 @@ RT_FLAG_KEEP_COUNTERS = 1 << 8
 RT_FLAG_ACCEL_BVH = 1 << 9
 RT_FLAG_COUNT_WORK = 1 << 10
 RT_FLAG_PILOT_SCHEDULE = 1 << 11  # launch expensive tiles first (4-spp pilot per frame geometry)
+RT_FLAG_LAYER_BVH = 1 << 12  # layer scenes: walk the layer BVH instead of the layer grid
 RT_CHUNK_SPP = 64  # include/rt.h: samples per chunk of the two-level pixel sum
 
 _f = ctypes.POINTER(ctypes.c_float)

@@ -16,7 +16,8 @@ from test_oracle import stat_compare
 
 pytestmark = pytest.mark.gpu
 
-ACCELS = {"scan": 0, "bvh": 1 << 9}  # RT_FLAG_ACCEL_BVH
+# RT_FLAG_ACCEL_BVH: layer scenes walk the layer grid; + RT_FLAG_LAYER_BVH: the layer BVH
+ACCELS = {"scan": 0, "bvh": 1 << 9, "layer_bvh": (1 << 9) | (1 << 12)}
 
 
 @pytest.fixture(params=list(ACCELS), ids=list(ACCELS))
@@ -121,11 +122,12 @@ def test_bvh_equals_scan_headline_frame(rtow, gpu_ctx):
     cam = rtow.camera_cpu(aspect=3840 / 2160)
     p = rtow.make_params(3840, 2160, 500, seed=3)
     a, sa = gpu_ctx.render(cam, p)
-    p.flags |= 1 << 9
-    b, sb = gpu_ctx.render(cam, p)
-    assert sa.segments == sb.segments
-    n_diff = int((a != b).sum())
-    assert n_diff == 0, n_diff
+    for acc in (ACCELS["bvh"], ACCELS["layer_bvh"]):  # the layer grid and the layer BVH
+        p.flags = acc
+        b, sb = gpu_ctx.render(cam, p)
+        assert sa.segments == sb.segments
+        n_diff = int((a != b).sum())
+        assert n_diff == 0, (acc, n_diff)
 
 
 def test_bvh_equals_scan_ten_thousand_spheres(rtow, gpu_ctx):
@@ -135,11 +137,12 @@ def test_bvh_equals_scan_ten_thousand_spheres(rtow, gpu_ctx):
     cam = rtow.camera_cpu(aspect=1920 / 1080)
     p = rtow.make_params(1920, 1080, 4, seed=21, flags=1 << 10)
     a, sa = gpu_ctx.render(cam, p)
-    p.flags |= 1 << 9
-    b, sb = gpu_ctx.render(cam, p)
-    assert sa.segments == sb.segments
-    assert np.array_equal(a, b)
-    assert sb.sphere_tests * 50 < sa.sphere_tests  # the BVH does >50x fewer sphere tests
+    for acc in (ACCELS["bvh"], ACCELS["layer_bvh"]):
+        p.flags = (1 << 10) | acc
+        b, sb = gpu_ctx.render(cam, p)
+        assert sa.segments == sb.segments
+        assert np.array_equal(a, b)
+        assert sb.sphere_tests * 50 < sa.sphere_tests  # >50x fewer sphere tests than the scan
 
 
 def test_empty_scene_all_sky(rtow, gpu_ctx, accel):
@@ -357,3 +360,29 @@ def test_bvh_layer_mode_boundary_bit_exact(rtow, gpu_ctx, n_big):
     b, sb = gpu_ctx.render(cam, p)
     assert sa.segments == sb.segments
     assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("view", ["grazing", "axis", "below", "inside"])
+def test_layer_grid_walk_edge_cases(rtow, gpu_ctx, view):
+    """The layer grid's per-lane DDA on the rays that stress it: a camera in the
+    layer looking along it (rays cross the whole grid, many nearly horizontal),
+    an axis-aligned view (direction components exactly 0 for the centre
+    column / row), a camera under the layer looking up through it, and one
+    inside the grid looking down.  Bit-exact vs the oracle at a small size;
+    grid == layer BVH == scan at a larger one."""
+    looks = {"grazing": ((12.0, 0.2, 1.3), (-11.0, 0.18, -1.0)),
+             "axis": ((0.0, 0.3, 14.0), (0.0, 0.3, 0.0)),
+             "below": ((0.5, -0.5, 0.5), (3.0, 2.0, 2.0)),
+             "inside": ((-2.0, 1.2, -3.0), (1.0, 0.0, 2.5))}[view]
+    scene = rtow.final_scene()
+    cam = rtow.camera_cpu(lookfrom=looks[0], lookat=looks[1], aspect=64 / 36)
+    p = rtow.make_params(64, 36, 5, seed=31)
+    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p, ACCELS["bvh"]))
+    cam = rtow.camera_cpu(lookfrom=looks[0], lookat=looks[1], aspect=480 / 270)
+    p = rtow.make_params(480, 270, 16, seed=32)
+    a, sa = gpu_ctx.render(cam, p)
+    for acc in (ACCELS["bvh"], ACCELS["layer_bvh"]):
+        p.flags = acc
+        b, sb = gpu_ctx.render(cam, p)
+        assert sa.segments == sb.segments
+        assert np.array_equal(a, b), (view, acc)
