@@ -33,7 +33,8 @@ sys.path.insert(0, PKG)
 
 PEAK_FP32_TFLOPS = 157.3      # MI355X vector fp32 (MI355X_MICROARCH.md, chip table)
 FLOPS_PER_TEST = 17           # algorithmic flops per ray-sphere test
-FLOPS_PER_BOX = 12            # slab test: 6 fma (2 flop) per ray-box test (BVH mode)
+FLOPS_PER_BOX = 12            # slab test: 6 fma (2 flop) per ray-box test (layer BVH walk)
+FLOPS_PER_CELL = 2            # layer grid walk: one compare + one add per DDA cell step
 # wave64 VALU issue ceiling: one independent v_fma_f32 per 1.041 ns per SIMD
 # with all 64 lanes active (tools/ubench_exec.hip on MI355X), 256 CUs x 4 SIMDs
 VALU_ISSUE_PEAK = 1024 / 1.041e-9  # wave instructions per second
@@ -60,9 +61,11 @@ def parse():
     ap.add_argument("--depth", type=int, default=50)
     ap.add_argument("--half-extent", type=int, default=11, help="11: 486 spheres; 50: 10k spheres")
     ap.add_argument("--row-block", type=int, default=8)
-    ap.add_argument("--accel", choices=["scan", "bvh"], default="bvh",
-                    help="bvh: wave-uniform BVH walk (default; bit-identical result to the scan, "
-                         "tested on the full headline frame); scan: brute-force closest hit")
+    ap.add_argument("--accel", choices=["scan", "bvh", "layer_bvh"], default="bvh",
+                    help="bvh: acceleration structures (default): the final scene is a layer "
+                         "scene, so the per-lane layer grid walk; layer_bvh: the wave-uniform "
+                         "layer BVH walk instead; scan: brute-force closest hit.  All three give "
+                         "the same image (tested on the full headline frame)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl (= RCCL over xGMI); gloo only to rehearse the multi-process path "
                          "on a one-GPU box (tiles staged through host memory)")
@@ -153,8 +156,10 @@ def main():
         # runs in the first (warmup) frame of this geometry; timed frames reuse
         # the order (include/rt.h RT_FLAG_PILOT_SCHEDULE)
         params.flags |= rtow.RT_FLAG_PILOT_SCHEDULE
-    if a.accel == "bvh":
+    if a.accel in ("bvh", "layer_bvh"):
         params.flags |= rtow.RT_FLAG_ACCEL_BVH
+    if a.accel == "layer_bvh":
+        params.flags |= rtow.RT_FLAG_LAYER_BVH
     tile = torch.zeros((params.local_rows, W, 3), dtype=torch.float32, device=dev)
     gdev = dev if a.backend == "nccl" else torch.device("cpu")
     gather_list = ([torch.empty(tile.shape, dtype=tile.dtype, device=gdev) for _ in range(world)]
@@ -230,7 +235,9 @@ def main():
             rtow.write_ppm(a.out, rtow.tonemap(frame, spp), binary=a.out.endswith((".p6", ".pnm")))
 
         k_avg_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-        flops = work.sphere_tests * FLOPS_PER_TEST + work.box_tests * FLOPS_PER_BOX
+        # box_tests counts slab tests (layer BVH) or DDA cell steps (layer grid)
+        flops = work.sphere_tests * FLOPS_PER_TEST + work.box_tests * (
+            FLOPS_PER_CELL if a.accel == "bvh" else FLOPS_PER_BOX)
         achieved = flops / k_avg_s / 1e12
         bf_achieved = work.bf_tests * FLOPS_PER_TEST / k_avg_s / 1e12
         value = segments / elapsed / 1e6
@@ -263,6 +270,8 @@ def main():
             "lane_efficiency": round(segments / (64.0 * wave_steps), 4) if wave_steps else None,
             "kernel_ms_avg_rank0": round(k_avg_s * 1e3, 3),
             "accel": a.accel,
+            "walk": {"bvh": "layer grid (per-lane DDA) + extras scanned", "scan": "brute force",
+                     "layer_bvh": "wave-uniform layer BVH + extras scanned"}[a.accel],
             "schedule": "launch order" if a.no_pilot else
                         "pilot (expensive tiles first; 4-spp pilot in the warmup frame)",
             "work_per_launch_rank0": {"segments": work.segments, "sphere_tests": work.sphere_tests,
@@ -280,7 +289,8 @@ def main():
                                                    "summary / this run's kernel time"}
                                         if valu_insts else None),
                          "note": "fp32 VALU-bound (no MFMA): executed ray-sphere tests x 17 flop "
-                                 "+ ray-box tests x 12 flop per launch / HIP-event kernel time; "
+                                 "+ grid cell steps x 2 flop (layer BVH: box tests x 12) per "
+                                 "launch / HIP-event kernel time; "
                                  "the kernel is control-heavy (min/max, compares, branches), so "
                                  "valu_issue is the bound it actually runs against"},
         }

@@ -15,5 +15,5 @@ timeout -s KILL 60 rocprofv3 -L > $out/counters_list.txt 2>&1 || true
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_INSTS_SALU SQ_INSTS_VALU --output-format csv -d $out/wait -o wait -- python3 $P > $out/wait.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc SQC_DCACHE_REQ SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES --output-format csv -d $out/sqc -o sqc -- python3 $P > $out/sqc.log 2>&1
 cd $GRAFT_REPO_ROOT
-python3 tools/pmc_traffic.py $out/wait $out/sqc --kernel "render_kernel<false, false, true, false>" --out $out/summary.json
+python3 tools/pmc_traffic.py $out/wait $out/sqc --kernel "${KERNEL:-render_kernel<false, false, true, false, true>}" --out $out/summary.json
 echo done
