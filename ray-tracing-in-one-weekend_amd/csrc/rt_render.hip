@@ -134,8 +134,10 @@ struct kparams {
   // item = (cx, cz, ks, original index bits).  nullptr: walk the layer BVH.
   const uint32_t *grid_cells;
   const f4 *grid_items;
-  float grid_x0, grid_z0, grid_x1, grid_z1, grid_g, grid_invg;
-  int grid_nx, grid_nz;
+  float grid_x0, grid_z0;  // corner of cell (0, 0), a ring cell
+  float grid_xi, grid_zi;  // inner box (the listed region): [xi, x1] x [zi, z1]
+  float grid_x1, grid_z1, grid_g, grid_invg;
+  int grid_nx, grid_nz;    // cells including the ring
 };
 
 // The kernel arguments, re-read from the kernarg segment (constant address
@@ -507,24 +509,30 @@ template <bool OPEN, bool STATS>
 __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz, float ta, float tb,
                                           const ray_pre &rl, hit_state &hs, work_ctr &wc) {
   const kparams p = kernargs();
-  const float ax = (p.grid_x0 - ox) * ix, bx = (p.grid_x1 - ox) * ix;
-  const float az = (p.grid_z0 - oz) * iz, bz = (p.grid_z1 - oz) * iz;
+  // clip to the grid's inner box (the cells around it are an empty ring)
+  const float ax = (p.grid_xi - ox) * ix, bx = (p.grid_x1 - ox) * ix;
+  const float az = (p.grid_zi - oz) * iz, bz = (p.grid_z1 - oz) * iz;
   ta = fmaxf(ta, fmaxf(fminf(ax, bx), fminf(az, bz)));
   tb = fminf(tb, fminf(fmaxf(ax, bx), fmaxf(az, bz)));
   if (!(ta <= tb)) return;
   const float dx = rl.dx.x, dz = rl.dz.x;
   const float px = fmaf(ta, dx, ox), pz = fmaf(ta, dz, oz);
-  int cx = min(max((int)floorf((px - p.grid_x0) * p.grid_invg), 0), p.grid_nx - 1);
-  int cz = min(max((int)floorf((pz - p.grid_z0) * p.grid_invg), 0), p.grid_nz - 1);
-  const int sx = dx < 0.0f ? -1 : 1, sz = dz < 0.0f ? -1 : 1;
-  float tmx = (fmaf((float)(cx + (dx < 0.0f ? 0 : 1)), p.grid_g, p.grid_x0) - ox) * ix;
-  float tmz = (fmaf((float)(cz + (dz < 0.0f ? 0 : 1)), p.grid_g, p.grid_z0) - oz) * iz;
+  const int nx = p.grid_nx, nz = p.grid_nz;
+  const int cx = min(max((int)floorf((px - p.grid_x0) * p.grid_invg), 1), nx - 2);
+  const int cz = min(max((int)floorf((pz - p.grid_z0) * p.grid_invg), 1), nz - 2);
+  // step directions from the sign of 1/d (= the sign bit of d, also for -0)
+  const bool nxs = ix < 0.0f, nzs = iz < 0.0f;
+  float tmx = (fmaf((float)(cx + (nxs ? 0 : 1)), p.grid_g, p.grid_x0) - ox) * ix;
+  float tmz = (fmaf((float)(cz + (nzs ? 0 : 1)), p.grid_g, p.grid_z0) - oz) * iz;
   const float tdx = p.grid_g * fabsf(ix), tdz = p.grid_g * fabsf(iz);
   const RT_GLOBAL uint32_t *__restrict__ cells = as_global(p.grid_cells);
   const RT_GLOBAL f4 *__restrict__ items = as_global(p.grid_items);
-  const int nx = p.grid_nx, nz = p.grid_nz;
+  // The walk stops on time alone: it leaves the inner box only at t ~ tb and
+  // the next boundary is a whole cell further, so it never steps past the ring.
+  int cell = cz * nx + cx;
+  const int dcx = nxs ? -1 : 1, dcz = nzs ? -nx : nx;
   while (true) {
-    const uint32_t ce = cells[cz * nx + cx];
+    const uint32_t ce = cells[(uint32_t)cell];
     const uint32_t first = ce >> 4, cnt = ce & 15u;
     if (STATS) ++wc.boxes;
     for (uint32_t k = 0; k < cnt; ++k) {
@@ -535,15 +543,17 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
       candidate<OPEN>(e >= it.z, h, e - it.z, __float_as_int(it.w), hs);
       if (STATS) ++wc.tests;
     }
-    if (fminf(tmx, tmz) > fminf(tb, hs.tmax)) break;
+    // v_min_f32 written out: fminf would first canonicalise all four operands
+    float tnext, lim;
+    asm("v_min_f32 %0, %1, %2" : "=v"(tnext) : "v"(tmx), "v"(tmz));
+    asm("v_min_f32 %0, %1, %2" : "=v"(lim) : "v"(tb), "v"(hs.tmax));
+    if (tnext > lim) break;
     if (tmx < tmz) {
-      cx += sx;
+      cell += dcx;
       tmx += tdx;
-      if ((unsigned)cx >= (unsigned)nx) break;
     } else {
-      cz += sz;
+      cell += dcz;
       tmz += tdz;
-      if ((unsigned)cz >= (unsigned)nz) break;
     }
   }
 }
@@ -952,7 +962,7 @@ struct rt_context {
   uint32_t extra_pair0 = 0, n_extra_pairs = 0;
   uint32_t *d_grid_cells = nullptr;  // layer grid (nullptr: none)
   float *d_grid_items = nullptr;
-  float grid_x0 = 0, grid_z0 = 0, grid_x1 = 0, grid_z1 = 0, grid_g = 0;
+  float grid_x0 = 0, grid_z0 = 0, grid_xi = 0, grid_zi = 0, grid_x1 = 0, grid_z1 = 0, grid_g = 0;
   int grid_nx = 0, grid_nz = 0;
   unsigned long long *d_counters = nullptr;
   float *d_frame = nullptr;
@@ -1253,7 +1263,7 @@ struct bvh_builder {
   // cells list at most 15 spheres (else g shrinks).
   std::vector<uint32_t> grid_cells;
   std::vector<float> grid_items;  // 4 floats per item
-  float grid_x0 = 0, grid_z0 = 0, grid_x1 = 0, grid_z1 = 0, grid_g = 0;
+  float grid_x0 = 0, grid_z0 = 0, grid_xi = 0, grid_zi = 0, grid_x1 = 0, grid_z1 = 0, grid_g = 0;
   int grid_nx = 0, grid_nz = 0;
   void build_grid(const rt_scene_view *s, uint32_t n_tree) {
     double x0 = 1e300, x1 = -1e300, z0 = 1e300, z1 = -1e300;
@@ -1291,10 +1301,14 @@ struct bvh_builder {
           }
       }
       if (!ok) continue;
-      grid_cells.assign((size_t)nx * nz, 0);
+      // stored with a ring of empty cells around the listed nx x nz (the
+      // kernel's DDA may step one cell past the listed region before it stops)
+      const int rx = nx + 2, rz = nz + 2;
+      grid_cells.assign((size_t)rx * rz, 0);
       grid_items.clear();
       for (size_t c = 0; c < lists.size(); ++c) {
-        grid_cells[c] = (uint32_t)(grid_items.size() / 4) << 4 | (uint32_t)lists[c].size();
+        const size_t rc = (c / nx + 1) * (size_t)rx + (c % nx + 1);
+        grid_cells[rc] = (uint32_t)(grid_items.size() / 4) << 4 | (uint32_t)lists[c].size();
         for (uint32_t i : lists[c]) {
           const double x = s->cx[i], y = s->cy[i], z = s->cz[i], r = s->radius[i];
           grid_items.push_back(s->cx[i]);
@@ -1311,11 +1325,13 @@ struct bvh_builder {
         grid_items.clear();
         return;
       }
-      grid_x0 = (float)x0;
-      grid_z0 = (float)z0;
+      grid_x0 = (float)(x0 - g);
+      grid_z0 = (float)(z0 - g);
+      grid_xi = (float)x0;
+      grid_zi = (float)z0;
       grid_g = (float)g;
-      grid_nx = nx;
-      grid_nz = nz;
+      grid_nx = rx;
+      grid_nz = rz;
       grid_x1 = (float)(x0 + nx * g);
       grid_z1 = (float)(z0 + nz * g);
       return;
@@ -1578,6 +1594,8 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
   c->extra_pair0 = bb.extra_pair0;
   c->n_extra_pairs = bb.n_extra_pairs;
   c->grid_x0 = bb.grid_x0;
+  c->grid_xi = bb.grid_xi;
+  c->grid_zi = bb.grid_zi;
   c->grid_z0 = bb.grid_z0;
   c->grid_x1 = bb.grid_x1;
   c->grid_z1 = bb.grid_z1;
@@ -1629,6 +1647,8 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
   kp.grid_cells = c->d_grid_cells;
   kp.grid_items = (const rtk::f4 *)c->d_grid_items;
   kp.grid_x0 = c->grid_x0;
+  kp.grid_xi = c->grid_xi;
+  kp.grid_zi = c->grid_zi;
   kp.grid_z0 = c->grid_z0;
   kp.grid_x1 = c->grid_x1;
   kp.grid_z1 = c->grid_z1;
