@@ -64,6 +64,12 @@ constexpr long long kSplitTilesPilot = 6LL * 256 * 4 * 8;
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+// STATS builds: the grid walk's box_hits counts wave-level DDA iterations, or
+// with RT_COUNT_ITEMS=1 wave-level item iterations (tools/grid_wave_counts.py)
+#ifndef RT_COUNT_ITEMS
+#define RT_COUNT_ITEMS 0
+#endif
+
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 // scan record for two consecutive spheres i, i+1 (32 B): every field is a
@@ -498,6 +504,14 @@ __device__ __forceinline__ int walk_step(const bvh_node &nd, int node, bool hit,
   return nd.skip;
 }
 
+// This lane's index in its wave, recomputed where it is needed (volatile: not
+// hoisted, so it is not held in a VGPR through the bounce loop).
+__device__ __forceinline__ int lane_now() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 // Per-lane 2-D DDA over the layer grid (layer mode): the lane visits the x-z
 // cells its own segment crosses inside the layer's y-slab, [ta, tb] clipped to
 // the grid box, in order, and tests the spheres listed in each cell with the
@@ -534,8 +548,14 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
   while (true) {
     const uint32_t ce = cells[(uint32_t)cell];
     const uint32_t first = ce >> 4, cnt = ce & 15u;
-    if (STATS) ++wc.boxes;
+    // STATS: boxes = lane-level cell visits; box_hits / roots = wave-level DDA
+    // / item iterations (counted once per wave, by its first active lane)
+    if (STATS) {
+      ++wc.boxes;
+      if (!RT_COUNT_ITEMS && lane_now() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true))) ++wc.box_hits;
+    }
     for (uint32_t k = 0; k < cnt; ++k) {
+      if (STATS && RT_COUNT_ITEMS && lane_now() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true))) ++wc.box_hits;
       const f4 it = items[first + k];
       const float h = fmaf(it.y, dz, fmaf(it.x, dx, rl.nk1.x));
       const float g = fmaf(it.y, rl.oz2.x, fmaf(it.x, rl.ox2.x, rl.o2.x));
@@ -670,13 +690,6 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
   return hs;
 }
 
-// This lane's index in its wave, recomputed where it is needed (volatile: not
-// hoisted, so it is not held in a VGPR through the bounce loop).
-__device__ __forceinline__ int lane_now() {
-  int l;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-  return l;
-}
 
 // 8 waves per SIMD (<= 64 VGPRs, 78 SGPRs).  The walk is a serial latency
 // chain per wave (scalar node load -> slab test -> ballot -> branch), so more
