@@ -517,8 +517,10 @@ __device__ __forceinline__ int lane_now() {
 // the grid box, in order, and tests the spheres listed in each cell with the
 // leaf test's arithmetic (NOY fold: same bits as scan_pairs).  It stops once
 // the next cell starts beyond min(tb, tmax).  Cell lists hold every sphere
-// whose padded box (the BVH's reach) comes within kGridPad of the cell, so
-// the fp32 DDA's boundary errors cannot skip a sphere the walk would test.
+// whose padded box (the BVH's reach) comes within the builder's pad of the
+// cell (bvh_builder::build_grid), so the fp32 DDA's boundary errors cannot
+// skip a sphere that could win.  Lanes walk independently: the wave runs
+// until its last lane is done.
 template <bool OPEN, bool STATS>
 __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz, float ta, float tb,
                                           const ray_pre &rl, hit_state &hs, work_ctr &wc) {
