@@ -65,7 +65,8 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 // STATS builds: the grid walk's box_hits counts wave-level DDA iterations, or
-// with RT_COUNT_ITEMS=1 wave-level item iterations (tools/grid_wave_counts.py)
+// with RT_COUNT_ITEMS=1 wave-level item iterations, =2 wave-level item
+// iterations that run the root sequence (tools/grid_wave_counts.py)
 #ifndef RT_COUNT_ITEMS
 #define RT_COUNT_ITEMS 0
 #endif
@@ -557,11 +558,14 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
       if (!RT_COUNT_ITEMS && lane_now() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true))) ++wc.box_hits;
     }
     for (uint32_t k = 0; k < cnt; ++k) {
-      if (STATS && RT_COUNT_ITEMS && lane_now() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true))) ++wc.box_hits;
+      if (STATS && RT_COUNT_ITEMS == 1 && lane_now() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true))) ++wc.box_hits;
       const f4 it = items[first + k];
       const float h = fmaf(it.y, dz, fmaf(it.x, dx, rl.nk1.x));
       const float g = fmaf(it.y, rl.oz2.x, fmaf(it.x, rl.ox2.x, rl.o2.x));
       const float e = fmaf(h, h, -g);
+      if (STATS && RT_COUNT_ITEMS == 2 && __builtin_amdgcn_ballot_w64(e >= it.z) &&
+          lane_now() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
+        ++wc.box_hits;
       candidate<OPEN>(e >= it.z, h, e - it.z, __float_as_int(it.w), hs);
       if (STATS) ++wc.tests;
     }
