@@ -386,3 +386,37 @@ def test_layer_grid_walk_edge_cases(rtow, gpu_ctx, view):
         b, sb = gpu_ctx.render(cam, p)
         assert sa.segments == sb.segments
         assert np.array_equal(a, b), (view, acc)
+
+
+@pytest.mark.parametrize("n_small", [80, 300])  # >= 64: layer mode; the grid builds / does not (> 15 per cell)
+def test_dense_layer_grid_build_paths(rtow, gpu_ctx, n_small):
+    """A dense layer (small spheres crowded into 1.5 x 1.5, overlapping): with 80
+    the grid builds (its cells may shrink to keep <= 15 spheres per cell); with
+    300 no cell size does, no grid is built and the layer BVH walks.  Either
+    way bit-exact vs the oracle, and equal to the scan."""
+    import dataclasses
+    rng = np.random.default_rng(n_small)
+    f32 = np.float32
+    n = n_small + 1
+    kind = np.array([0] + [int(k) for k in rng.integers(0, 3, n_small)], np.uint32)
+    base = rtow.final_scene()
+    scene = dataclasses.replace(
+        base,
+        cx=np.array([0.0] + list(rng.uniform(-0.75, 0.75, n_small)), f32),
+        cy=np.array([-1000.0] + [0.2] * n_small, f32),
+        cz=np.array([0.0] + list(rng.uniform(-0.75, 0.75, n_small)), f32),
+        radius=np.array([1000.0] + [0.2] * n_small, f32),
+        kind=kind,
+        albedo=rng.uniform(0.2, 0.9, (n, 3)).astype(f32),
+        param=np.where(kind == 2, 1.5, 0.3).astype(f32))
+    cam = rtow.camera_cpu(lookfrom=(3.0, 1.5, 2.0), lookat=(0.0, 0.1, 0.0), aspect=64 / 36)
+    p = rtow.make_params(64, 36, 5, seed=41)
+    assert_bit_exact(*gpu_vs_oracle(rtow, gpu_ctx, scene, cam, p, ACCELS["bvh"]))
+    cam = rtow.camera_cpu(lookfrom=(3.0, 1.5, 2.0), lookat=(0.0, 0.1, 0.0), aspect=320 / 180)
+    p = rtow.make_params(320, 180, 16, seed=42)
+    a, sa = gpu_ctx.render(cam, p)
+    for acc in (ACCELS["bvh"], ACCELS["layer_bvh"]):
+        p.flags = acc
+        b, sb = gpu_ctx.render(cam, p)
+        assert sa.segments == sb.segments
+        assert np.array_equal(a, b), (n_small, acc)
