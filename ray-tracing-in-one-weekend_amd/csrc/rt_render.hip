@@ -523,12 +523,15 @@ __device__ __forceinline__ int lane_now() {
 // skip a sphere that could win.  Lanes walk independently: the wave runs
 // until its last lane is done.
 template <bool OPEN, bool STATS>
-__device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz, float ta, float tb,
-                                          const ray_pre &rl, hit_state &hs, work_ctr &wc) {
+__device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz, float oix, float oiz,
+                                          float ta, float tb, const ray_pre &rl, hit_state &hs,
+                                          work_ctr &wc) {
   const kparams p = kernargs();
-  // clip to the grid's inner box (the cells around it are an empty ring)
-  const float ax = (p.grid_xi - ox) * ix, bx = (p.grid_x1 - ox) * ix;
-  const float az = (p.grid_zi - oz) * iz, bz = (p.grid_z1 - oz) * iz;
+  // clip to the grid's inner box (the cells around it are an empty ring);
+  // slab times as fma(x, 1/d, -o/d) like the BVH's (the ring and the cell
+  // lists' pad absorb the rounding)
+  const float ax = fmaf(p.grid_xi, ix, oix), bx = fmaf(p.grid_x1, ix, oix);
+  const float az = fmaf(p.grid_zi, iz, oiz), bz = fmaf(p.grid_z1, iz, oiz);
   ta = fmaxf(ta, fmaxf(fminf(ax, bx), fminf(az, bz)));
   tb = fminf(tb, fminf(fmaxf(ax, bx), fmaxf(az, bz)));
   if (!(ta <= tb)) return;
@@ -539,8 +542,8 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
   const int cz = min(max((int)floorf((pz - p.grid_z0) * p.grid_invg), 1), nz - 2);
   // step directions from the sign of 1/d (= the sign bit of d, also for -0)
   const bool nxs = ix < 0.0f, nzs = iz < 0.0f;
-  float tmx = (fmaf((float)(cx + (nxs ? 0 : 1)), p.grid_g, p.grid_x0) - ox) * ix;
-  float tmz = (fmaf((float)(cz + (nzs ? 0 : 1)), p.grid_g, p.grid_z0) - oz) * iz;
+  float tmx = fmaf(fmaf((float)(cx + (nxs ? 0 : 1)), p.grid_g, p.grid_x0), ix, oix);
+  float tmz = fmaf(fmaf((float)(cz + (nzs ? 0 : 1)), p.grid_g, p.grid_z0), iz, oiz);
   const float tdx = p.grid_g * fabsf(ix), tdz = p.grid_g * fabsf(iz);
   const RT_GLOBAL uint32_t *__restrict__ cells = as_global(p.grid_cells);
   const RT_GLOBAL f4 *__restrict__ items = as_global(p.grid_items);
@@ -651,7 +654,7 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
         ray_pre rg = rp;
         rg.nk1 = fma2(f2{p.layer_cy, p.layer_cy}, rp.dy, rp.nk1);
         rg.o2 = fma2(f2{p.layer_cy, p.layer_cy}, rp.oy2, rp.o2);
-        if (tyl_n <= tyl_fc) grid_walk<OPEN, STATS>(ox, oz, ix, iz, tyl_n, tyl_fc, rg, hs, wc);
+        if (tyl_n <= tyl_fc) grid_walk<OPEN, STATS>(ox, oz, ix, iz, oix, oiz, tyl_n, tyl_fc, rg, hs, wc);
         return hs;
       }
       // a wave none of whose rays crosses the layer before tmax skips the walk
