@@ -60,6 +60,10 @@ constexpr long long kSplitTiles = 12LL * 256 * 4 * 7;
 // 1/2 share (64 800 tiles) 151 ms unsplit vs 154 split, a 1/4 share (32 400)
 // 87 unsplit vs 78 split, 1/8 40 ms split (tools/rank_times.py --pilot).
 constexpr long long kSplitTilesPilot = 6LL * 256 * 4 * 8;
+// ... and, in pilot order, 4 waves per tile's chunks are enough: with the
+// layer grid a 1/4 share (32 400 tiles) runs 47.4 ms at units 4 vs 48.2 / 48.5
+// at 2 / 8, a 1/8 share 24.7 ms at 4 or 8 (29.7 at 2).
+constexpr int kPilotUnits = 4;
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -1708,8 +1712,10 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
   // time, so the chunks are split over `units` waves (tools/rank_times.py).
   const int n_chunks = std::max(1, (prm->spp + RT_CHUNK_SPP - 1) / RT_CHUNK_SPP);
   long long units = prm->units;
-  if (units <= 0)
-    units = tiles < ((prm->flags & RT_FLAG_PILOT_SCHEDULE) ? rtk::kSplitTilesPilot : rtk::kSplitTiles) ? n_chunks : 1;
+  if (units <= 0) {
+    const bool pilot = (prm->flags & RT_FLAG_PILOT_SCHEDULE) != 0;
+    units = tiles < (pilot ? rtk::kSplitTilesPilot : rtk::kSplitTiles) ? (pilot ? rtk::kPilotUnits : n_chunks) : 1;
+  }
   if (prm->spp <= 0 || prm->max_depth <= 0) units = 1;  // nothing is traced
   units = std::max(1LL, std::min<long long>(units, n_chunks));
   const int cpu = (int)((n_chunks + units - 1) / units);
