@@ -632,12 +632,16 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
     const float iz = __builtin_amdgcn_rcpf(fabsf(dz) < 1e-18f ? copysignf(1e-18f, dz) : dz);
     const float oix = -ox * ix, oiy = -oy * iy, oiz = -oz * iz;
     // the wave walks the DFS order of its majority direction octant, so
-    // coherent rays visit near children first and tmax culls the rest
-    const uint32_t half = __builtin_popcountll(__builtin_amdgcn_ballot_w64(true)) / 2;
-    const int oct = (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dx < 0.0f)) > half ? 1 : 0) |
-                    (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dy < 0.0f)) > half ? 2 : 0) |
-                    (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dz < 0.0f)) > half ? 4 : 0);
-    const RT_CONST bvh_node *__restrict__ order = nodes + (size_t)oct * p.n_nodes;
+    // coherent rays visit near children first and tmax culls the rest (BVH
+    // walks only: the grid build never computes it)
+    auto walk_order = [&]() {
+      const uint32_t half = __builtin_popcountll(__builtin_amdgcn_ballot_w64(true)) / 2;
+      const int oct = (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dx < 0.0f)) > half ? 1 : 0) |
+                      (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dy < 0.0f)) > half ? 2 : 0) |
+                      (__builtin_popcountll(__builtin_amdgcn_ballot_w64(dz < 0.0f)) > half ? 4 : 0);
+      return nodes + (size_t)oct * p.n_nodes;
+    };
+    const RT_CONST bvh_node *__restrict__ order = GRID ? nullptr : walk_order();
     if (p.layer_mode) {
       // the spheres off the layer (in the final scene the ground and the three
       // big spheres) are scanned first: their hits shorten tmax for the walk
@@ -684,7 +688,7 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
         asm("v_min3_f32 %0, %1, %2, %3" : "=v"(tf) : "v"(tf2.x), "v"(tf2.y), "v"(tyl_fc));
         node = walk_step<OPEN, STATS, true>(nd, node, tn <= tf, geom, orig, rl, hs, wc, tyl_f, tyl_fc);
       }
-    } else {
+    } else if (!GRID) {  // (the grid build runs on layer scenes only)
       const f2 vix = {ix, ix}, viy = {iy, iy}, viz = {iz, iz};
       const f2 vox = {oix, oix}, voy = {oiy, oiy}, voz = {oiz, oiz};
       int node = 0;
