@@ -273,15 +273,20 @@ __device__ __forceinline__ float cbrt01(float u) {
   return u == 0.0f ? 0.0f : c;
 }
 
-// uniform direction on the unit sphere (replaces the rejection loop of
-// random_unit_vector, src/cpu/vec3.h:105-114; equal in distribution)
-__device__ __forceinline__ void unit_vec(float u1, float u2, float &x, float &y, float &z) {
-  z = fmaf(-2.0f, u1, 1.0f);
-  float r = sqrt_k(fmaf(-z, z, 1.0f));
+// (rho cos 2 pi u, rho sin 2 pi u), rho = sqrt_k(a): the polar draw of both
+//  * the uniform direction on the unit sphere (z = 1 - 2 u1, a = 1 - z^2,
+//    u = u2; replaces the rejection loop of random_unit_vector,
+//    src/cpu/vec3.h:105-114, equal in distribution), and
+//  * camera_ray's lens-disk sample (a = u3, u = u4).
+// The render loop runs it once per lane and step for whichever of the two the
+// lane needs (a wave whose lanes both bounce and start new paths would
+// otherwise run it twice).
+__device__ __forceinline__ void polar(float a, float u, float &x, float &y) {
+  const float rho = sqrt_k(a);
   float s, c;
-  sincos_turn(u2, s, c);
-  x = r * c;
-  y = r * s;
+  sincos_turn(u, s, c);
+  x = rho * c;
+  y = rho * s;
 }
 
 // x * 1/|x| with 1/|x| from an integer-seeded inverse square root and three
@@ -305,9 +310,11 @@ __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, fl
 }
 
 // camera ray for (pixel, sample): get_ray, src/cpu/camera.h:28-34 (model CPU)
-// or src/gpu/camera.h:153-167 (model GPU); r = pcg4d(pix, sample, 0, seed32)
-__device__ __forceinline__ void camera_ray(const kparams &p, const uint4 r, int col, int grow,
-                                           float &ox, float &oy, float &oz,
+// or src/gpu/camera.h:153-167 (model GPU), from r = pcg4d(pix, sample, 0,
+// seed32) and the lens sample (ddx, ddy) = polar(unif(r.z), unif(r.w)) (used
+// only when the camera has a lens); the direction is left unnormalised
+__device__ __forceinline__ void camera_dir(const kparams &p, const uint4 r, float ddx, float ddy,
+                                           int col, int grow, float &ox, float &oy, float &oz,
                                            float &dx, float &dy, float &dz) {
   float u1 = unif(r.x), u2 = unif(r.y);
   float fs, ft;
@@ -326,10 +333,6 @@ __device__ __forceinline__ void camera_ray(const kparams &p, const uint4 r, int 
   oy = p.cam.eye[1];
   oz = p.cam.eye[2];
   if (p.cam.has_lens) {
-    float rr = sqrt_k(unif(r.z));
-    float s, c;
-    sincos_turn(unif(r.w), s, c);
-    float ddx = rr * c, ddy = rr * s;
     ox = fmaf(ddy, p.cam.lens_v[0], fmaf(ddx, p.cam.lens_u[0], ox));
     oy = fmaf(ddy, p.cam.lens_v[1], fmaf(ddx, p.cam.lens_u[1], oy));
     oz = fmaf(ddy, p.cam.lens_v[2], fmaf(ddx, p.cam.lens_u[2], oz));
@@ -337,6 +340,15 @@ __device__ __forceinline__ void camera_ray(const kparams &p, const uint4 r, int 
   dx = tx - ox;
   dy = ty - oy;
   dz = tz - oz;
+}
+
+// the whole camera ray for r = pcg4d(pix, sample, 0, seed32)
+__device__ __forceinline__ void camera_ray(const kparams &p, const uint4 r, int col, int grow,
+                                           float &ox, float &oy, float &oz,
+                                           float &dx, float &dy, float &dz) {
+  float ddx = 0.0f, ddy = 0.0f;
+  if (p.cam.has_lens) polar(unif(r.z), unif(r.w), ddx, ddy);
+  camera_dir(p, r, ddx, ddy, col, grow, ox, oy, oz, dx, dy, dz);
   normalize3(dx, dy, dz);
 }
 
@@ -786,6 +798,11 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
       // it is used; only absorbed paths need a second hash below)
       const bool miss = best < 0;
       const uint4 r = pcg4d(pix, miss ? sample : sample - 1u, miss ? 0u : (uint32_t)(depth + 1), q.seed32);
+      // one polar draw per lane and step: a hit's unit vector (oracle unit_vec:
+      // z = 1 - 2 u1), a miss's lens sample for its next camera ray
+      const float uz = fmaf(-2.0f, unif(r.x), 1.0f);
+      float ux, uy;
+      polar(miss ? unif(r.z) : fmaf(-uz, uz, 1.0f), unif(miss ? r.w : r.y), ux, uy);
 
       bool path_done = false;
       if (miss) {
@@ -815,8 +832,6 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         const float dn = dot3(dx, dy, dz, nx, ny, nz);
         const float k2 = -2.0f * dn;  // reflect(d, n) = d - 2 (d.n) n, vec3.h:122
         const float rx = fmaf(k2, nx, dx), ry = fmaf(k2, ny, dy), rz = fmaf(k2, nz, dz);
-        float ux, uy, uz;
-        unit_vec(unif(r.x), unif(r.y), ux, uy, uz);
         float sx, sy, sz;
         bool scattered = true;
         if (sr.kind == RT_LAMBERTIAN) {
@@ -901,8 +916,13 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           int col, grow;
           pixel_cr(k, col, grow);
           uint4 rc = r;
-          if (!miss) rc = pcg4d(pix, sample, 0u, k.seed32);  // absorbed or depth limit
-          camera_ray(k, rc, col, grow, ox, oy, oz, dx, dy, dz);
+          float ddx = ux, ddy = uy;  // a miss's lens sample, drawn above
+          if (!miss) {  // absorbed or depth limit: the camera draw needs its own hash
+            rc = pcg4d(pix, sample, 0u, k.seed32);
+            if (k.cam.has_lens) polar(unif(rc.z), unif(rc.w), ddx, ddy);
+          }
+          camera_dir(k, rc, ddx, ddy, col, grow, ox, oy, oz, dx, dy, dz);
+          normalize3(dx, dy, dz);
           ++sample;
           depth = 0;
           thr = thg = thb = 1.0f;
