@@ -887,10 +887,9 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           ox = px;
           oy = py;
           oz = pz;
-          dx = sx;
+          dx = sx;  // normalised below, with the new camera rays
           dy = sy;
           dz = sz;
-          normalize3(dx, dy, dz);
         }
       }
       if (path_done) {
@@ -922,7 +921,6 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
             if (k.cam.has_lens) polar(unif(rc.z), unif(rc.w), ddx, ddy);
           }
           camera_dir(k, rc, ddx, ddy, col, grow, ox, oy, oz, dx, dy, dz);
-          normalize3(dx, dy, dz);
           ++sample;
           depth = 0;
           thr = thg = thb = 1.0f;
@@ -930,6 +928,9 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           alive = false;
         }
       }
+      // one normalize3 per lane and step: the bounce direction or the new
+      // camera ray's (a finished lane's is unused)
+      normalize3(dx, dy, dz);
     }
   }
 
