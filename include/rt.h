@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 typedef enum {
   RT_OK = 0,
@@ -67,8 +67,9 @@ enum {
   RT_FLAG_COUNT_WORK = 1u << 10,
   /* scheduling, not semantics: launch the most expensive tiles first.  The
    * first render of a new frame geometry (size, band, camera, flags) runs a
-   * 4-spp pilot that measures every tile's segments and synchronises the
-   * stream once to sort them; later renders reuse the order. */
+   * 4-spp pilot that measures every tile's segments and sorts the blocks on
+   * the device (enqueued, no host sync); later renders reuse the order
+   * (DESIGN.md 6). */
   RT_FLAG_PILOT_SCHEDULE = 1u << 11,
   /* acceleration, not semantics (with RT_FLAG_ACCEL_BVH): when the scene is a
    * thin layer of like spheres plus a few others, rt_scene_upload builds an
@@ -208,14 +209,19 @@ int rt_scene_upload(rt_context *ctx, const rt_scene_view *scene);
 /* Enqueue the render kernel on `stream` (a hipStream_t, NULL = the context's
  * own stream) writing params->width * params->local_rows * 3 floats to the
  * DEVICE pointer accum_rgb.  Replaces render<<<>>> (src/gpu/camera.h:169-195).
- * Does not synchronise.  Segment counters are read by rt_collect_stats after
- * the stream has completed. */
+ * Does not synchronise, also not on the first render of a frame geometry
+ * with RT_FLAG_PILOT_SCHEDULE (the pilot and its sort are enqueued too).
+ * Renders of one context on different streams run one after another (each
+ * waits for the previous one's event): they share the context's scratch
+ * buffers.  Segment counters are read by rt_collect_stats after the stream has
+ * completed. */
 int rt_render_async(rt_context *ctx, const rt_camera *cam, const rt_params *params,
                     float *accum_rgb, void *stream);
 
 /* Synchronous convenience: render into a context-owned device buffer, time the
  * kernel with hipEvents, copy the sums to HOST memory host_rgb
- * (width*local_rows*3 floats) and fill stats (may be NULL). */
+ * (width*local_rows*3 floats) and fill stats (may be NULL).  kernel_ms spans
+ * the render kernel (and the chunk fold), not a first-frame pilot. */
 int rt_render(rt_context *ctx, const rt_camera *cam, const rt_params *params,
               float *host_rgb, rt_stats *stats);
 
@@ -229,12 +235,45 @@ int rt_reset_stats(rt_context *ctx, void *stream);
 /* ---- output (write_color src/cpu/color.h:8-23, output_image
  *      src/gpu/camera.h:197-210) ---- */
 
+/* tonemap arithmetic: the two references' write_color */
+typedef enum {
+  RT_TONEMAP_CPU = 0, /* src/cpu/color.h:8-23: scale = 1.0/spp, sqrt, clamp in fp64 */
+  RT_TONEMAP_GPU = 1  /* src/gpu/color.h:16-38: scale = 1.0f/spp, sqrtf, clamp in fp32 */
+} rt_tonemap_mode;
+
 /* int(256 * clamp(sqrt(sum/spp), 0, 0.999)) per channel, fp64 like src/cpu. */
 int rt_tonemap_u8(const float *sums_rgb, size_t n_pixels, int spp, uint8_t *out_rgb);
 
+/* The same on the host in either arithmetic (RT_TONEMAP_GPU: the fp32 levels of
+ * src/gpu's output_image, which can differ by one from the fp64 ones on a level
+ * boundary).  Threaded for large frames. */
+int rt_tonemap_u8_mode(const float *sums_rgb, size_t n_pixels, int spp, int mode, uint8_t *out_rgb);
+
+/* write_color on the DEVICE: d_sums (3 * n_pixels fp32 sums, e.g. a frame tile
+ * from rt_render_async) -> d_out (3 * n_pixels bytes), enqueued on `stream`
+ * (NULL = the context's stream).  Bit-identical to rt_tonemap_u8_mode with
+ * the same mode.  Lets a multi-GPU render gather bytes (3 B per pixel) instead
+ * of fp32 sums (12 B). */
+int rt_tonemap_async(rt_context *ctx, const float *d_sums, size_t n_pixels, int spp, int mode,
+                     uint8_t *d_out, void *stream);
+
 /* "P3\nW H\n255\n" + one "r g b\n" line per pixel (binary P6 if binary!=0).
- * Rows are written top to bottom, as both references do. */
+ * Rows are written top to bottom, as both references do.  Streams: P3 text is
+ * formatted in bounded chunks by several threads and written in order (no
+ * whole-file buffer), so a 16384 x 16384 frame needs megabytes, not 3 GB. */
 int rt_write_ppm(int fd, const uint8_t *rgb, int width, int height, int binary);
+
+/* ---- diagnostics ---- */
+
+/* Known-answer evaluation of the render kernel's own device arithmetic on
+ * `device` (synchronous).  10 doubles in, 9 out per case (layouts in
+ * rt_render.hip, kat_kernel):
+ *   RT_KAT_SPHERE_HIT   sphere::hit            src/cpu/sphere.h:24-51
+ *   RT_KAT_REFLECT      reflect                src/cpu/vec3.h:122-124
+ *   RT_KAT_REFRACT      refract                src/cpu/vec3.h:126-131
+ *   RT_KAT_REFLECTANCE  dielectric::reflectance src/cpu/material.h:82-87 */
+enum { RT_KAT_SPHERE_HIT = 0, RT_KAT_REFLECT = 1, RT_KAT_REFRACT = 2, RT_KAT_REFLECTANCE = 3 };
+int rt_device_kat(int device, int kind, const double *in, size_t n_cases, double *out);
 
 #ifdef __cplusplus
 }

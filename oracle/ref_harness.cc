@@ -19,9 +19,14 @@
 //
 // Usage:
 //   ref_harness scene                       -> scene dump (%.17g), then "next <rnd>"
-//   ref_harness render W ASPN ASPD SPP [DEPTH] [scene=final|five] [SKIP]
+//   ref_harness render W ASPN ASPD SPP [DEPTH] [scene=final|five|file:PATH] [SKIP]
+//                      [APERTURE FOCUS_DIST]
 //        SKIP = number of random_double() draws discarded after the scene is
 //        built (an independent stream, for the oracle's own noise floor)
+//        file:PATH = spheres read from a dump in `scene`'s format (e.g. the
+//        10 000-sphere stress scene), built with the reference's own
+//        sphere / lambertian / metal / dielectric classes
+//        APERTURE FOCUS_DIST override the camera's lens (depth of field)
 //        PPM (P3) on stdout; on stderr a JSON stats line with samples,
 //        segments (= hittable_list::hit calls), sphere_tests and seconds.
 //   ref_harness kat                         -> known-answer vectors (JSON lines)
@@ -104,6 +109,28 @@ hittable_list five_scene() {
   return world;
 }
 
+// "K cx cy cz r a0 a1 a2 param" per line (K = L | M | D), as dump_world prints
+hittable_list file_scene(const char *path) {
+  hittable_list world;
+  FILE *f = std::fopen(path, "r");
+  if (!f) {
+    std::fprintf(stderr, "cannot open %s\n", path);
+    std::exit(2);
+  }
+  char k[8];
+  double c[3], r, a[3], p;
+  while (std::fscanf(f, "%7s %lf %lf %lf %lf %lf %lf %lf %lf", k, &c[0], &c[1], &c[2], &r, &a[0], &a[1], &a[2],
+                     &p) == 9) {
+    shared_ptr<material> m;
+    if (k[0] == 'L') m = make_shared<lambertian>(color(a[0], a[1], a[2]));
+    else if (k[0] == 'M') m = make_shared<metal>(color(a[0], a[1], a[2]), p);
+    else m = make_shared<dielectric>(p);
+    world.add(make_shared<sphere>(point3(c[0], c[1], c[2]), r, m));
+  }
+  std::fclose(f);
+  return world;
+}
+
 int cmd_scene() {
   auto world = random_scene();
   dump_world(world);
@@ -130,8 +157,14 @@ int cmd_render(int argc, char **argv) {
     lookat = point3(0, 0, -1);
     aperture = 0.0;
     dist_to_focus = 3.4;
+  } else if (scene.compare(0, 5, "file:") == 0) {
+    world = file_scene(scene.c_str() + 5);
   } else {
     world = random_scene();
+  }
+  if (argc > 10) {
+    aperture = std::atof(argv[9]);
+    dist_to_focus = std::atof(argv[10]);
   }
   for (long long k = 0; k < skip; ++k) (void)random_double();
   vec3 vup(0, 1, 0);

@@ -30,6 +30,7 @@
 #include <cstring>
 #include <random>
 #include <thread>
+#include <cstdlib>
 #include <vector>
 
 namespace {
@@ -657,7 +658,15 @@ int rto_kernel_render(const rt_scene_view *scene, const rt_camera *cam, const rt
   const kscene sc = make_kscene(*scene);
   kctx k{&sc, cam, p, (uint32_t)p->seed ^ ((uint32_t)(p->seed >> 32) * 0x9E3779B9u),
          (p->flags & RT_FLAG_OPEN_INTERVAL) != 0, (p->flags & RT_FLAG_METAL_UNIT_VECTOR) != 0};
-  if (threads < 1) threads = (int)std::max(1u, std::thread::hardware_concurrency());
+  if (threads < 1) {
+    // the machine's cores, but no more than OMP_NUM_THREADS (16 on the GPU
+    // box, whose nproc shows the whole host) or 16
+    threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (const char *e = std::getenv("OMP_NUM_THREADS")) {
+      const int k = std::atoi(e);
+      if (k >= 1) threads = std::min(threads, k);
+    }
+  }
   std::atomic<int> next_row{0};
   std::atomic<unsigned long long> total{0};
   auto worker = [&]() {

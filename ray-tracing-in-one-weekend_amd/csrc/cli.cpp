@@ -16,8 +16,9 @@
 //   --camera cpu|gpu --semantics cpu|gpu --accel bvh|scan --gpus N --device N
 //   --gather rccl|host --out FILE --p6 --quiet
 // With --gpus N > 1 the frame is split into interleaved 8-row bands, one
-// context and stream per device, and the tiles are gathered to device 0 with
-// one RCCL ncclGather over xGMI (single process, ncclCommInitAll); device 0's
+// context and stream per device; each device tonemaps its tile to bytes
+// (rt_tonemap_async) and the byte tiles are gathered to device 0 with one
+// RCCL ncclGather over xGMI (single process, ncclCommInitAll); device 0's
 // gathered frame is copied to the host once.  --gather host copies each tile
 // back instead (no RCCL); --gather rccl forces the RCCL path also on 1 GPU.
 #include <fcntl.h>
@@ -77,9 +78,7 @@ void check(int st, const char *what) {
 struct gpu_job {
   int device;
   rt_params params;
-  std::vector<float> host;
   rt_stats stats{};
-  int status = RT_OK;
 };
 
 }  // namespace
@@ -157,15 +156,21 @@ int main(int argc, char **argv) {
   if (ndev < 1) die("no HIP device", RT_ERR_NO_DEVICE);
   if (o.gpus > ndev) o.gpus = ndev;
 
+  // the reference's stderr surface, per personality (src/cpu/main.cc:103-105,
+  // src/gpu/main.cu:121-125); our extra lines follow the timing
   if (!o.quiet) {
     std::fprintf(stderr, "Image Size = %d x %d\n", o.width, o.height);
     std::fprintf(stderr, "Samples Per Pixel = %d\n", o.spp);
-    std::fprintf(stderr, "Number of GPUs = %d (wave64 tiles of 8 x 8 pixels)\n", o.gpus);
-    std::fprintf(stderr, "Spheres = %u\n", buf.n);
-    if (gpu_mode || o.seed_set) std::fprintf(stderr, "Random Seed = %llu\n", o.seed);
+    if (gpu_mode) {
+      std::fprintf(stderr, "Block Dim (a x b threads) = %d x %d\n", 8, 8);  // one wave64 per 8x8 tile
+      std::fprintf(stderr, "Random Seed = %llu\n", o.seed);
+    } else {
+      std::fprintf(stderr, "Number of CPU threads = %d\n", 1);  // one host thread drives the GPUs
+      if (o.seed_set) std::fprintf(stderr, "Random Seed = %llu\n", o.seed);
+    }
   }
 
-  // ---- render: one context per GPU, interleaved row bands ----
+  // ---- render: one context and stream per GPU, interleaved row bands ----
   const int row_block = 8;
   std::vector<gpu_job> jobs(o.gpus);
   for (int g = 0; g < o.gpus; ++g) {
@@ -193,7 +198,6 @@ int main(int argc, char **argv) {
     }
     jobs[g].device = o.gpus == 1 ? o.device : g;
     jobs[g].params = p;
-    jobs[g].host.resize(3 * (size_t)p.width * p.local_rows);
   }
   std::vector<rt_context *> ctxs(o.gpus, nullptr);
   for (int g = 0; g < o.gpus; ++g) {
@@ -201,15 +205,23 @@ int main(int argc, char **argv) {
     check(rt_scene_upload(ctxs[g], &view), "rt_scene_upload");
   }
   const bool use_rccl = o.gather == "rccl" || (o.gather == "auto" && o.gpus > 1);
-  std::vector<float> gathered;  // rccl: device 0's tiles, rank-major
-  std::chrono::high_resolution_clock::time_point start, end;
+  // Every device renders its tile (fp32 sums) and tonemaps it on the device
+  // (write_color, src/cpu/color.h or src/gpu/color.h by personality) into 3 B
+  // per pixel; the byte tiles are gathered to device 0 with one RCCL
+  // ncclGather over xGMI (or copied back one by one with --gather host) and
+  // written by the streaming PPM writer: the host never holds fp32 sums.
+  const int tone_mode = (o.flags & RT_FLAG_GPU_SEMANTICS) == RT_FLAG_GPU_SEMANTICS ? RT_TONEMAP_GPU
+                                                                                 : RT_TONEMAP_CPU;
+  const size_t tile_px = (size_t)o.width * jobs[0].params.local_rows;
+  std::vector<int> devs(o.gpus);
+  for (int g = 0; g < o.gpus; ++g) devs[g] = jobs[g].device;
+  std::vector<hipStream_t> streams(o.gpus);
+  std::vector<float *> d_tile(o.gpus, nullptr);
+  std::vector<uint8_t *> d_u8(o.gpus, nullptr);
+  uint8_t *d_all = nullptr;
+  std::vector<ncclComm_t> comms;
   if (use_rccl) {
-    // every device renders its tile on its own stream (launches are
-    // asynchronous: one host thread), then one ncclGather to device 0
-    const size_t tile = 3 * (size_t)o.width * jobs[0].params.local_rows;
-    std::vector<int> devs(o.gpus);
-    for (int g = 0; g < o.gpus; ++g) devs[g] = jobs[g].device;
-    std::vector<ncclComm_t> comms(o.gpus);
+    comms.resize(o.gpus);
     // RCCL prints a version banner on stdout, which carries the PPM: send it
     // to stderr while the communicators are created
     std::fflush(stdout);
@@ -220,58 +232,55 @@ int main(int argc, char **argv) {
     ::dup2(saved_stdout, 1);
     ::close(saved_stdout);
     if (init != ncclSuccess) die("ncclCommInitAll", RT_ERR_HIP);
-    std::vector<hipStream_t> streams(o.gpus);
-    std::vector<float *> d_tile(o.gpus, nullptr);
-    float *d_all = nullptr;
-    for (int g = 0; g < o.gpus; ++g) {
-      if (hipSetDevice(devs[g]) != hipSuccess || hipStreamCreateWithFlags(&streams[g], hipStreamNonBlocking) != hipSuccess ||
-          hipMalloc(&d_tile[g], tile * sizeof(float)) != hipSuccess)
-        die("device buffers", RT_ERR_HIP);
-      if (g == 0 && hipMalloc(&d_all, tile * o.gpus * sizeof(float)) != hipSuccess) die("gather buffer", RT_ERR_HIP);
-    }
-    for (int g = 0; g < o.gpus; ++g) {
-      (void)hipSetDevice(devs[g]);
-      (void)hipDeviceSynchronize();
-    }
-    start = std::chrono::high_resolution_clock::now();
-    for (int g = 0; g < o.gpus; ++g)
-      check(rt_render_async(ctxs[g], &cam, &jobs[g].params, d_tile[g], streams[g]), "rt_render_async");
+  }
+  for (int g = 0; g < o.gpus; ++g) {
+    if (hipSetDevice(devs[g]) != hipSuccess ||
+        hipStreamCreateWithFlags(&streams[g], hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&d_tile[g], 3 * tile_px * sizeof(float)) != hipSuccess ||
+        hipMalloc(&d_u8[g], 3 * tile_px) != hipSuccess)
+      die("device buffers", RT_ERR_HIP);
+    if (use_rccl && g == 0 && hipMalloc(&d_all, 3 * tile_px * o.gpus) != hipSuccess)
+      die("gather buffer", RT_ERR_HIP);
+  }
+  for (int g = 0; g < o.gpus; ++g) {
+    (void)hipSetDevice(devs[g]);
+    (void)hipDeviceSynchronize();
+  }
+  const auto start = std::chrono::high_resolution_clock::now();
+  for (int g = 0; g < o.gpus; ++g) {
+    check(rt_render_async(ctxs[g], &cam, &jobs[g].params, d_tile[g], streams[g]), "rt_render_async");
+    check(rt_tonemap_async(ctxs[g], d_tile[g], tile_px, o.spp > 0 ? o.spp : 1, tone_mode, d_u8[g], streams[g]),
+          "rt_tonemap_async");
+  }
+  if (use_rccl) {
     if (ncclGroupStart() != ncclSuccess) die("ncclGroupStart", RT_ERR_HIP);
     for (int g = 0; g < o.gpus; ++g)
-      if (ncclGather(d_tile[g], g == 0 ? d_all : nullptr, tile, ncclFloat32, 0, comms[g], streams[g]) != ncclSuccess)
+      if (ncclGather(d_u8[g], g == 0 ? d_all : nullptr, 3 * tile_px, ncclUint8, 0, comms[g], streams[g]) !=
+          ncclSuccess)
         die("ncclGather", RT_ERR_HIP);
     if (ncclGroupEnd() != ncclSuccess) die("ncclGroupEnd", RT_ERR_HIP);
-    for (int g = 0; g < o.gpus; ++g) {
-      (void)hipSetDevice(devs[g]);
-      if (hipStreamSynchronize(streams[g]) != hipSuccess) die("render + gather", RT_ERR_HIP);
-    }
-    end = std::chrono::high_resolution_clock::now();
-    gathered.resize(tile * o.gpus);
-    (void)hipSetDevice(devs[0]);
-    if (hipMemcpy(gathered.data(), d_all, gathered.size() * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess)
-      die("gather copy", RT_ERR_HIP);
-    for (int g = 0; g < o.gpus; ++g) {
-      check(rt_collect_stats(ctxs[g], &jobs[g].stats), "rt_collect_stats");
-      (void)hipSetDevice(devs[g]);
-      (void)hipFree(d_tile[g]);
-      (void)hipStreamDestroy(streams[g]);
-      ncclCommDestroy(comms[g]);
-    }
-    (void)hipSetDevice(devs[0]);
-    (void)hipFree(d_all);
-  } else {
-    start = std::chrono::high_resolution_clock::now();
-    std::vector<std::thread> threads;
-    for (int g = 0; g < o.gpus; ++g)
-      threads.emplace_back([&, g]() {
-        jobs[g].status = rt_render(ctxs[g], &cam, &jobs[g].params, jobs[g].host.data(), &jobs[g].stats);
-      });
-    for (auto &t : threads) t.join();
-    end = std::chrono::high_resolution_clock::now();
-    for (int g = 0; g < o.gpus; ++g) check(jobs[g].status, "rt_render");
   }
+  for (int g = 0; g < o.gpus; ++g) {
+    (void)hipSetDevice(devs[g]);
+    if (hipStreamSynchronize(streams[g]) != hipSuccess) die("render", RT_ERR_HIP);
+  }
+  const auto end = std::chrono::high_resolution_clock::now();
+  // byte tiles, rank-major, to the host
+  std::vector<uint8_t> tiles(3 * tile_px * o.gpus);
+  if (use_rccl) {
+    (void)hipSetDevice(devs[0]);
+    if (hipMemcpy(tiles.data(), d_all, tiles.size(), hipMemcpyDeviceToHost) != hipSuccess)
+      die("gather copy", RT_ERR_HIP);
+  } else {
+    for (int g = 0; g < o.gpus; ++g) {
+      (void)hipSetDevice(devs[g]);
+      if (hipMemcpy(&tiles[3 * tile_px * g], d_u8[g], 3 * tile_px, hipMemcpyDeviceToHost) != hipSuccess)
+        die("tile copy", RT_ERR_HIP);
+    }
+  }
+  for (int g = 0; g < o.gpus; ++g) check(rt_collect_stats(ctxs[g], &jobs[g].stats), "rt_collect_stats");
 
-  // main.cu:134-139 timing lines
+  // main.cu:134-139 / main.cc:125-130 timing lines
   float ms = std::chrono::duration<float, std::milli>(end - start).count();
   int time_cost_in_ms = (int)(ms + 0.999f);
   int time_cost_in_sec = (time_cost_in_ms + 999) / 1000;
@@ -281,27 +290,27 @@ int main(int argc, char **argv) {
     samples += j.stats.samples;
   }
   if (!o.quiet) {
-    std::fprintf(stderr, "Time Cost (ms) = %d ms\n", time_cost_in_ms);
+    if (!gpu_mode) std::fprintf(stderr, "\rScanlines remaining: %d ", 0);  // main.cc:112, all rendered at once
+    std::fprintf(stderr, "%sTime Cost (ms) = %d ms\n", gpu_mode ? "" : "\n", time_cost_in_ms);
     std::fprintf(stderr, "Time Cost (sec) = %d sec\n", time_cost_in_sec);
+    std::fprintf(stderr, "Number of GPUs = %d, spheres = %u\n", o.gpus, buf.n);
     std::fprintf(stderr, "Throughput = %.1f Mray/s, %.1f Msample/s (%llu segments)\n",
                  segs / (ms * 1e3), samples / (ms * 1e3), segs);
   }
 
-  // ---- assemble + tonemap + PPM (output_image, src/gpu/camera.h:197-210) ----
-  std::vector<float> frame(3 * (size_t)o.width * o.height, 0.0f);
+  // ---- assemble rows + PPM (output_image, src/gpu/camera.h:197-210) ----
+  std::vector<uint8_t> rgb(3 * (size_t)o.width * o.height, 0);
   for (int g = 0; g < o.gpus; ++g) {
     const rt_params &p = jobs[g].params;
-    const float *src = use_rccl ? &gathered[3 * (size_t)o.width * p.local_rows * g] : jobs[g].host.data();
+    const uint8_t *src = &tiles[3 * tile_px * g];
     for (int r = 0; r < p.local_rows; ++r) {
       const int band = r / p.row_block;
       const int grow = (band * p.band_stride + p.band_offset) * p.row_block + r % p.row_block;
       if (grow >= o.height) continue;
-      std::memcpy(&frame[3 * (size_t)grow * o.width], &src[3 * (size_t)r * o.width], 3 * sizeof(float) * o.width);
+      std::memcpy(&rgb[3 * (size_t)grow * o.width], &src[3 * (size_t)r * o.width], 3 * (size_t)o.width);
     }
   }
-  std::vector<uint8_t> rgb(frame.size());
-  check(rt_tonemap_u8(frame.data(), (size_t)o.width * o.height, o.spp > 0 ? o.spp : 1, rgb.data()),
-        "rt_tonemap_u8");
+  std::vector<uint8_t>().swap(tiles);
   int fd = 1;
   if (!o.out.empty()) {
     fd = ::open(o.out.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
@@ -309,7 +318,18 @@ int main(int argc, char **argv) {
   }
   check(rt_write_ppm(fd, rgb.data(), o.width, o.height, o.p6 ? 1 : 0), "rt_write_ppm");
   if (fd != 1) ::close(fd);
+  for (int g = 0; g < o.gpus; ++g) {
+    (void)hipSetDevice(devs[g]);
+    (void)hipFree(d_tile[g]);
+    (void)hipFree(d_u8[g]);
+    (void)hipStreamDestroy(streams[g]);
+    if (use_rccl) ncclCommDestroy(comms[g]);
+  }
+  if (d_all) {
+    (void)hipSetDevice(devs[0]);
+    (void)hipFree(d_all);
+  }
   for (auto *c : ctxs) rt_context_destroy(c);
-  if (!o.quiet) std::fprintf(stderr, "\nDone.\n");
+  if (!o.quiet && !gpu_mode) std::fprintf(stderr, "\nDone.\n");  // main.cc:132
   return 0;
 }

@@ -9,12 +9,14 @@
 // produce a different 484-sphere scene -- SURVEY 0.2 / 8a-1).
 #include "rt.h"
 
+#include <algorithm>
 #include <cerrno>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <random>
 #include <string>
+#include <thread>
 #include <unistd.h>
 #include <vector>
 
@@ -243,50 +245,132 @@ int rt_camera_gpu(const double lookfrom[3], const double lookat[3],
   return RT_OK;
 }
 
-int rt_tonemap_u8(const float *sums_rgb, size_t n_pixels, int spp, uint8_t *out_rgb) {
-  if ((!sums_rgb || !out_rgb) && n_pixels) return RT_ERR_INVALID;
-  if (spp < 1) return RT_ERR_INVALID;
-  // write_color, src/cpu/color.h:8-23, in fp64
-  const double scale = 1.0 / spp;
-  for (size_t i = 0; i < 3 * n_pixels; ++i) {
-    double x = std::sqrt(scale * (double)sums_rgb[i]);
-    if (x < 0.0) x = 0.0;
-    if (x > 0.999) x = 0.999;
-    if (!(x == x)) x = 0.0;  // NaN sums (never produced) map to 0
-    out_rgb[i] = (uint8_t)(int)(256 * x);
-  }
-  return RT_OK;
+}  // extern "C"
+
+namespace {
+
+// host worker count for the output helpers: at most 16 threads, one per
+// ~4 M channels, 1 for small frames
+unsigned host_threads(size_t work) {
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  return (unsigned)std::max<size_t>(1, std::min<size_t>({(size_t)hw, (size_t)16, work >> 22}));
 }
 
-int rt_write_ppm(int fd, const uint8_t *rgb, int width, int height, int binary) {
-  if (fd < 0 || width < 0 || height < 0 || (!rgb && width && height)) return RT_ERR_INVALID;
-  std::string buf;
-  buf.reserve(binary ? (size_t)width * height * 3 + 32 : (size_t)width * height * 12 + 32);
-  // both references print "P3\nW H\n255\n" (src/cpu/main.cc:109,
-  // src/gpu/camera.h:201)
-  buf += binary ? "P6\n" : "P3\n";
-  buf += std::to_string(width) + " " + std::to_string(height) + "\n255\n";
-  const size_t n = (size_t)width * height;
-  if (binary) {
-    buf.append(reinterpret_cast<const char *>(rgb), 3 * n);
-  } else {
-    char line[16];
-    for (size_t i = 0; i < n; ++i) {
-      int len = std::snprintf(line, sizeof line, "%d %d %d\n", rgb[3 * i], rgb[3 * i + 1],
-                              rgb[3 * i + 2]);
-      buf.append(line, (size_t)len);
-    }
+template <class F>
+void parallel_ranges(size_t n, F f) {
+  const unsigned t = host_threads(n);
+  if (t <= 1) {
+    f((size_t)0, n);
+    return;
   }
-  const char *p = buf.data();
-  size_t left = buf.size();
+  std::vector<std::thread> th;
+  for (unsigned k = 0; k < t; ++k) th.emplace_back(f, n * k / t, n * (k + 1) / t);
+  for (auto &x : th) x.join();
+}
+
+// write_color, src/cpu/color.h:8-23 (fp64)
+inline uint8_t level_cpu(float s, double scale) {
+  double x = std::sqrt(scale * (double)s);
+  if (x < 0.0) x = 0.0;
+  if (x > 0.999) x = 0.999;
+  if (!(x == x)) x = 0.0;  // NaN sums (never produced) map to 0
+  return (uint8_t)(int)(256 * x);
+}
+
+// write_color, src/gpu/color.h:16-38 (fp32: r *= 1.0f/spp, sqrtf, interval(0, 0.999f).clamp)
+inline uint8_t level_gpu(float s, float scale) {
+  float x = std::sqrt(s * scale);
+  if (x < 0.000f) x = 0.000f;
+  if (x > 0.999f) x = 0.999f;
+  if (!(x == x)) x = 0.0f;
+  return (uint8_t)(int)(256.0f * x);
+}
+
+bool write_all(int fd, const char *p, size_t left) {
   while (left) {
     ssize_t k = ::write(fd, p, left);
     if (k < 0) {
       if (errno == EINTR) continue;
-      return RT_ERR_IO;
+      return false;
     }
     p += k;
     left -= (size_t)k;
+  }
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_tonemap_u8_mode(const float *sums_rgb, size_t n_pixels, int spp, int mode, uint8_t *out_rgb) {
+  if ((!sums_rgb || !out_rgb) && n_pixels) return RT_ERR_INVALID;
+  if (spp < 1 || (mode != RT_TONEMAP_CPU && mode != RT_TONEMAP_GPU)) return RT_ERR_INVALID;
+  const double scale = 1.0 / spp;
+  const float scale_f = 1.0f / (float)spp;
+  parallel_ranges(3 * n_pixels, [&](size_t b, size_t e) {
+    if (mode == RT_TONEMAP_CPU)
+      for (size_t i = b; i < e; ++i) out_rgb[i] = level_cpu(sums_rgb[i], scale);
+    else
+      for (size_t i = b; i < e; ++i) out_rgb[i] = level_gpu(sums_rgb[i], scale_f);
+  });
+  return RT_OK;
+}
+
+int rt_tonemap_u8(const float *sums_rgb, size_t n_pixels, int spp, uint8_t *out_rgb) {
+  return rt_tonemap_u8_mode(sums_rgb, n_pixels, spp, RT_TONEMAP_CPU, out_rgb);
+}
+
+int rt_write_ppm(int fd, const uint8_t *rgb, int width, int height, int binary) {
+  if (fd < 0 || width < 0 || height < 0 || (!rgb && width && height)) return RT_ERR_INVALID;
+  // both references print "P3\nW H\n255\n" (src/cpu/main.cc:109,
+  // src/gpu/camera.h:201)
+  const std::string head = std::string(binary ? "P6\n" : "P3\n") + std::to_string(width) + " " +
+                           std::to_string(height) + "\n255\n";
+  if (!write_all(fd, head.data(), head.size())) return RT_ERR_IO;
+  const size_t n = (size_t)width * height;
+  if (binary) return write_all(fd, reinterpret_cast<const char *>(rgb), 3 * n) ? RT_OK : RT_ERR_IO;
+  // P3: "r g b\n" per pixel (color.h:20-22).  Chunks of kChunk pixels are
+  // formatted by up to 16 threads into their own buffers and written in
+  // order; memory stays at threads x kChunk x 12 bytes whatever the frame.
+  static constexpr size_t kChunk = 1 << 16;
+  struct digits {
+    char c[4];
+    uint8_t len;
+  };
+  static const std::vector<digits> tab = [] {
+    std::vector<digits> t(256);
+    for (int v = 0; v < 256; ++v) t[v].len = (uint8_t)std::snprintf(t[v].c, 4, "%d", v);
+    return t;
+  }();
+  auto format = [&](size_t b, size_t e, std::string &out) {
+    out.resize(12 * (e - b));
+    char *p = &out[0];
+    for (size_t i = b; i < e; ++i) {
+      for (int k = 0; k < 3; ++k) {
+        const digits &d = tab[rgb[3 * i + k]];
+        std::memcpy(p, d.c, 4);  // (the table entry is padded; only len bytes count)
+        p += d.len;
+        *p++ = k < 2 ? ' ' : '\n';
+      }
+    }
+    out.resize((size_t)(p - out.data()));
+  };
+  const size_t n_chunks = (n + kChunk - 1) / kChunk;
+  const unsigned t = (unsigned)std::max<size_t>(1, std::min<size_t>(host_threads(3 * n), n_chunks));
+  std::vector<std::string> buf(t);
+  for (size_t c0 = 0; c0 < n_chunks; c0 += t) {
+    const size_t m = std::min<size_t>(t, n_chunks - c0);
+    auto job = [&](size_t j) { format((c0 + j) * kChunk, std::min(n, (c0 + j + 1) * kChunk), buf[j]); };
+    if (m == 1) {
+      job(0);
+    } else {
+      std::vector<std::thread> th;
+      for (size_t j = 0; j < m; ++j) th.emplace_back(job, j);
+      for (auto &x : th) x.join();
+    }
+    for (size_t j = 0; j < m; ++j)
+      if (!write_all(fd, buf[j].data(), buf[j].size())) return RT_ERR_IO;
   }
   return RT_OK;
 }

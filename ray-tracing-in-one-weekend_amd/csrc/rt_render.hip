@@ -41,6 +41,8 @@
 #include "rt.h"
 
 extern "C" void rt_internal_set_hip_error(int e);
+extern "C" hipError_t rt_internal_block_order(const uint32_t *tile_cost, uint32_t blocks, uint32_t units,
+                                              uint32_t *order, hipStream_t st);
 
 namespace rtk {
 
@@ -307,6 +309,36 @@ __device__ __forceinline__ void normalize3(float &x, float &y, float &z) {
 
 __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {
   return fmaf(az, bz, fmaf(ay, by, ax * bx));
+}
+
+// reflect(v, n) = v - 2 dot(v, n) n (src/cpu/vec3.h:122-124), dn = dot(v, n)
+__device__ __forceinline__ void reflect3(float vx, float vy, float vz, float nx, float ny, float nz, float dn,
+                                         float &rx, float &ry, float &rz) {
+  const float k2 = -2.0f * dn;
+  rx = fmaf(k2, nx, vx);
+  ry = fmaf(k2, ny, vy);
+  rz = fmaf(k2, nz, vz);
+}
+
+// refract(uv, n, ratio) (src/cpu/vec3.h:126-131) with cos_t = fminf(-dot(uv, n), 1):
+// perp = ratio (uv + cos_t n), parallel = -sqrt(|1 - |perp|^2|) n
+__device__ __forceinline__ void refract3(float vx, float vy, float vz, float nx, float ny, float nz, float cos_t,
+                                         float ratio, float &sx, float &sy, float &sz) {
+  const float qx = ratio * fmaf(cos_t, nx, vx);
+  const float qy = ratio * fmaf(cos_t, ny, vy);
+  const float qz = ratio * fmaf(cos_t, nz, vz);
+  const float m = -sqrt_k(fabsf(1.0f - dot3(qx, qy, qz, qx, qy, qz)));
+  sx = fmaf(m, nx, qx);
+  sy = fmaf(m, ny, qy);
+  sz = fmaf(m, nz, qz);
+}
+
+// Schlick's reflectance (src/cpu/material.h:82-87), r0 = ((1 - ref_idx) / (1 +
+// ref_idx))^2 precomputed in fp64 (the same for ior and 1 / ior)
+__device__ __forceinline__ float schlick(float cosine, float r0) {
+  const float x = 1.0f - cosine;
+  const float x2 = x * x;
+  return fmaf(1.0f - r0, x2 * x2 * x, r0);
 }
 
 // camera ray for (pixel, sample): get_ray, src/cpu/camera.h:28-34 (model CPU)
@@ -830,8 +862,8 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         // shared by the material branches (computed once: lanes of one wave
         // usually hit several materials, so the branches all execute)
         const float dn = dot3(dx, dy, dz, nx, ny, nz);
-        const float k2 = -2.0f * dn;  // reflect(d, n) = d - 2 (d.n) n, vec3.h:122
-        const float rx = fmaf(k2, nx, dx), ry = fmaf(k2, ny, dy), rz = fmaf(k2, nz, dz);
+        float rx, ry, rz;
+        reflect3(dx, dy, dz, nx, ny, nz, dn, rx, ry, rz);
         float sx, sy, sz;
         bool scattered = true;
         if (sr.kind == RT_LAMBERTIAN) {
@@ -859,21 +891,12 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           const float cos_t = fminf(-dn, 1.0f);
           const float sin_t = sqrt_k(fmaf(-cos_t, cos_t, 1.0f));
           const bool cannot = ratio * sin_t > 1.0f;
-          const float x = 1.0f - cos_t;
-          const float x2 = x * x;
-          const float refl = fmaf(1.0f - sr.r0, x2 * x2 * x, sr.r0);
-          if (cannot || refl > unif(r.x)) {
+          if (cannot || schlick(cos_t, sr.r0) > unif(r.x)) {
             sx = rx;
             sy = ry;
             sz = rz;
           } else {
-            const float qx = ratio * fmaf(cos_t, nx, dx);
-            const float qy = ratio * fmaf(cos_t, ny, dy);
-            const float qz = ratio * fmaf(cos_t, nz, dz);
-            const float m = -sqrt_k(fabsf(1.0f - dot3(qx, qy, qz, qx, qy, qz)));
-            sx = fmaf(m, nx, qx);
-            sy = fmaf(m, ny, qy);
-            sz = fmaf(m, nz, qz);
+            refract3(dx, dy, dz, nx, ny, nz, cos_t, ratio, sx, sy, sz);
           }
         }
         // attenuation = albedo (dielectrics store 1,1,1: the product is exact)
@@ -994,6 +1017,125 @@ __global__ __launch_bounds__(256) void fold_chunks(const float *__restrict__ chu
   }
 }
 
+// Known-answer evaluation of the render kernel's own device arithmetic
+// (rt_device_kat; tests/test_parity_gpu.py checks it against the reference's
+// vectors in tests/golden/kat.jsonl).  Case layout: 10 doubles in, 9 out.
+//   RT_KAT_SPHERE_HIT  in  o[3] d[3] c[3] r      (sphere::hit, src/cpu/sphere.h:24-51,
+//                                                  t_min 0.001, t_max inf)
+//                      out hit, t (in units of the given d), p[3], normal[3], front_face
+//                      -- the scan's candidate test, refine_root, the shading normal
+//                      and set_face_normal, exactly as render_kernel runs them on a
+//                      direction normalised by normalize3
+//   RT_KAT_REFLECT     in  v[3] n[3]             out reflect3(v, n)
+//   RT_KAT_REFRACT     in  v[3] n[3] eta         out refract3(v, n, eta)
+//   RT_KAT_REFLECTANCE in  cosine ref_idx        out schlick(cosine, r0(ref_idx))
+__global__ __launch_bounds__(64) void kat_kernel(int kind, const double *__restrict__ in, int n,
+                                                 double *__restrict__ out) {
+  const int i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= n) return;
+  const double *a = in + 10 * (size_t)i;
+  double *o = out + 9 * (size_t)i;
+  for (int k = 0; k < 9; ++k) o[k] = 0.0;
+  if (kind == RT_KAT_SPHERE_HIT) {
+    const float ox = (float)a[0], oy = (float)a[1], oz = (float)a[2];
+    float dx = (float)a[3], dy = (float)a[4], dz = (float)a[5];
+    const double len = sqrt(a[3] * a[3] + a[4] * a[4] + a[5] * a[5]);
+    normalize3(dx, dy, dz);
+    shade_rec sr;
+    sr.cx = (float)a[6];
+    sr.cy = (float)a[7];
+    sr.cz = (float)a[8];
+    sr.radius = (float)a[9];
+    sr.inv_r = 1.0f / sr.radius;
+    const double cx = sr.cx, cy = sr.cy, cz = sr.cz, rr = sr.radius;
+    sr.ks = (float)(cx * cx + cy * cy + cz * cz - rr * rr);  // as rt_scene_upload
+    const float nk1 = -dot3(ox, oy, oz, dx, dy, dz);
+    const float o2 = dot3(ox, oy, oz, ox, oy, oz);
+    const float ox2 = -2.0f * ox, oy2 = -2.0f * oy, oz2 = -2.0f * oz;
+    const float h = fmaf(sr.cz, dz, fmaf(sr.cx, dx, fmaf(sr.cy, dy, nk1)));
+    const float g = fmaf(sr.cz, oz2, fmaf(sr.cx, ox2, fmaf(sr.cy, oy2, o2)));
+    const float e = fmaf(h, h, -g);
+    hit_state hs{__builtin_huge_valf(), -1, 1};
+    candidate<false>(e >= sr.ks, h, e - sr.ks, 0, hs);
+    if (hs.best < 0) return;
+    const float t = refine_root(sr, hs.tmax, hs.near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2);
+    const float px = fmaf(t, dx, ox), py = fmaf(t, dy, oy), pz = fmaf(t, dz, oz);
+    float nx = (px - sr.cx) * sr.inv_r, ny = (py - sr.cy) * sr.inv_r, nz = (pz - sr.cz) * sr.inv_r;
+    const bool front = (hs.near != 0) != (sr.inv_r < 0.0f);
+    if (!front) {
+      nx = -nx;
+      ny = -ny;
+      nz = -nz;
+    }
+    o[0] = 1.0;
+    o[1] = (double)t / len;
+    o[2] = px;
+    o[3] = py;
+    o[4] = pz;
+    o[5] = nx;
+    o[6] = ny;
+    o[7] = nz;
+    o[8] = front ? 1.0 : 0.0;
+  } else if (kind == RT_KAT_REFLECT || kind == RT_KAT_REFRACT) {
+    const float vx = (float)a[0], vy = (float)a[1], vz = (float)a[2];
+    const float nx = (float)a[3], ny = (float)a[4], nz = (float)a[5];
+    float x, y, z;
+    if (kind == RT_KAT_REFLECT) {
+      reflect3(vx, vy, vz, nx, ny, nz, dot3(vx, vy, vz, nx, ny, nz), x, y, z);
+    } else {
+      const float cos_t = fminf(-dot3(vx, vy, vz, nx, ny, nz), 1.0f);
+      refract3(vx, vy, vz, nx, ny, nz, cos_t, (float)a[6], x, y, z);
+    }
+    o[0] = x;
+    o[1] = y;
+    o[2] = z;
+  } else if (kind == RT_KAT_REFLECTANCE) {
+    const double r0 = (1.0 - a[1]) / (1.0 + a[1]);  // as rt_scene_upload's shade_rec.r0
+    o[0] = schlick((float)a[0], (float)(r0 * r0));
+  }
+}
+
+// write_color on the device (rt_tonemap_async): the level of a channel is
+// (int)(256 * clamp(sqrt(sum * scale), 0, 0.999)) in fp64 with scale = 1.0 / spp
+// (src/cpu/color.h:8-23), or in fp32 with scale = 1.0f / spp
+// (src/gpu/color.h:16-38).  sqrt is monotone, so the level is the number of
+// thresholds T[k] = min{q : sqrt_rn(q) >= k / 256}, k = 1..255, that q = sum *
+// scale reaches (tonemap_thresholds, on the host with its correctly rounded
+// sqrt).  The device estimates the level with its own sqrt and corrects it by
+// one step against T: the result does not depend on how the device rounds
+// sqrt.  NaN sums map to 0 (rt_tonemap_u8 does the same).  Four channels per
+// lane: one 16-B load, one 4-B store (HBM-bound, 15 B per pixel).
+template <bool FP32, typename T>
+__device__ __forceinline__ uint32_t tone_level(float s, T scale, const T *__restrict__ thr) {
+  const T q = (T)s * scale;
+  const T y = (T)256 * (FP32 ? (T)sqrtf((float)q) : (T)sqrt((double)q));
+  int l = y >= (T)255 ? 255 : (y > (T)0 ? (int)y : 0);
+  if (l < 255 && q >= thr[l + 1]) ++l;
+  else if (l > 0 && q < thr[l]) --l;
+  return (uint32_t)l;
+}
+
+template <bool FP32, typename T>
+__global__ __launch_bounds__(256) void tonemap_kernel(const float *__restrict__ sums, uint64_t n, T scale,
+                                                      const T *__restrict__ thr_g, uint8_t *__restrict__ out) {
+  __shared__ T thr[256];
+  thr[threadIdx.x] = thr_g[threadIdx.x];
+  __syncthreads();
+  const uint64_t n4 = n / 4;
+  const bool vec = ((uintptr_t)sums % 16 == 0) && ((uintptr_t)out % 4 == 0);
+  const uint64_t stride = (uint64_t)gridDim.x * 256u;
+  if (vec) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n4; i += stride) {
+      const f4 v = reinterpret_cast<const f4 *>(sums)[i];
+      reinterpret_cast<uint32_t *>(out)[i] =
+          tone_level<FP32, T>(v.x, scale, thr) | tone_level<FP32, T>(v.y, scale, thr) << 8 |
+          tone_level<FP32, T>(v.z, scale, thr) << 16 | tone_level<FP32, T>(v.w, scale, thr) << 24;
+    }
+  }
+  for (uint64_t i = (vec ? 4 * n4 : 0) + (uint64_t)blockIdx.x * 256u + threadIdx.x; i < n; i += stride)
+    out[i] = (uint8_t)tone_level<FP32, T>(sums[i], scale, thr);
+}
+
 }  // namespace rtk
 
 // ------------------------------------------------------------ context ----
@@ -1026,6 +1168,17 @@ struct rt_context {
   size_t chunk_floats = 0;
   uint64_t last_samples = 0;
   bool last_stats = false;
+  // Renders of one context may be enqueued on different streams; they share
+  // the scratch buffers above (chunk sums, block order), so each render first
+  // waits for the previous one: ev_done is recorded after every render on
+  // last_stream, and a render on another stream waits on it (no host sync).
+  hipEvent_t ev_done = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool have_done = false;
+  double tonemap_thr64[257];  // rt_tonemap_async level thresholds (see tonemap_thresholds)
+  float tonemap_thr32[257];
+  double *d_thr64 = nullptr;
+  float *d_thr32 = nullptr;
 };
 
 namespace {
@@ -1033,6 +1186,26 @@ namespace {
 int hip_fail(hipError_t e) {
   rt_internal_set_hip_error((int)e);
   return RT_ERR_HIP;
+}
+
+// T[k] = the smallest q >= 0 whose correctly rounded square root reaches
+// k / 256 (k = 1..255; T[0] unused), in fp64 and in fp32.  (k / 256)^2 is
+// exact in both; step down while the square root still rounds up to k / 256.
+void tonemap_thresholds(double *t64, float *t32) {
+  t64[0] = 0.0;
+  t32[0] = 0.0f;
+  for (int k = 1; k < 256; ++k) {
+    const double x = k / 256.0;
+    double q = x * x;
+    while (q > 0.0 && std::sqrt(std::nextafter(q, 0.0)) >= x) q = std::nextafter(q, 0.0);
+    t64[k] = q;
+    const float xf = (float)k / 256.0f;
+    float qf = xf * xf;
+    while (qf > 0.0f && std::sqrt(std::nextafter(qf, 0.0f)) >= xf) qf = std::nextafter(qf, 0.0f);
+    t32[k] = qf;
+  }
+  t64[256] = INFINITY;
+  t32[256] = INFINITY;
 }
 
 #define RT_HIP(call)                         \
@@ -1081,9 +1254,14 @@ struct bvh_builder {
     const char *v = std::getenv(name);
     return v ? std::max(lo, std::min(hi, std::atoi(v))) : dflt;
   }
-  static double env_double(const char *name, double dflt) {
+  // experiment knobs: only a finite value in [lo, hi] is taken, anything else
+  // (unset, garbage, 0, negative, NaN, inf) keeps the default
+  static double env_double(const char *name, double dflt, double lo = 0.01, double hi = 100.0) {
     const char *v = std::getenv(name);
-    return v ? std::atof(v) : dflt;
+    if (!v) return dflt;
+    char *end = nullptr;
+    const double x = std::strtod(v, &end);
+    return (end != v && std::isfinite(x) && x >= lo && x <= hi) ? x : dflt;
   }
 
   double area(const box &b) const {
@@ -1330,8 +1508,7 @@ struct bvh_builder {
     z0 -= 2 * pad;
     x1 += 2 * pad;
     z1 += 2 * pad;
-    double scale = 1.0;
-    if (const char *e = getenv("RTOW_GRID_SCALE")) scale = atof(e);
+    const double scale = env_double("RTOW_GRID_SCALE", 1.0, 0.05, 20.0);
     double g = scale * std::sqrt((x1 - x0) * (z1 - z0) / (double)n_tree);
     for (int attempt = 0; attempt < 8; ++attempt, g *= 0.8) {
       const int nx = (int)std::ceil((x1 - x0) / g), nz = (int)std::ceil((z1 - z0) / g);
@@ -1548,7 +1725,13 @@ int rt_context_create(int device_ordinal, rt_context **out) {
     if ((e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)) != hipSuccess) break;
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) break;
     if ((e = hipEventCreate(&c->ev1)) != hipSuccess) break;
+    if ((e = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming)) != hipSuccess) break;
     if ((e = hipMalloc(&c->d_counters, 8 * sizeof(unsigned long long))) != hipSuccess) break;
+    tonemap_thresholds(c->tonemap_thr64, c->tonemap_thr32);
+    if ((e = hipMalloc(&c->d_thr64, sizeof c->tonemap_thr64)) != hipSuccess) break;
+    if ((e = hipMalloc(&c->d_thr32, sizeof c->tonemap_thr32)) != hipSuccess) break;
+    if ((e = hipMemcpy(c->d_thr64, c->tonemap_thr64, sizeof c->tonemap_thr64, hipMemcpyHostToDevice)) != hipSuccess) break;
+    if ((e = hipMemcpy(c->d_thr32, c->tonemap_thr32, sizeof c->tonemap_thr32, hipMemcpyHostToDevice)) != hipSuccess) break;
   } while (0);
   if (e != hipSuccess) {
     st = hip_fail(e);
@@ -1570,6 +1753,9 @@ void rt_context_destroy(rt_context *c) {
   (void)hipFree(c->d_frame);
   (void)hipFree(c->d_chunks);
   (void)hipFree(c->d_order);
+  (void)hipFree(c->d_thr64);
+  (void)hipFree(c->d_thr32);
+  if (c->ev_done) (void)hipEventDestroy(c->ev_done);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1656,15 +1842,19 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
   return RT_OK;
 }
 
-int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, float *accum_rgb,
-                    void *stream) {
-  if (!c || !cam || !params_ok(prm) || (!accum_rgb && prm->local_rows && prm->width))
-    return RT_ERR_INVALID;
-  if (cam->model != RT_CAMERA_CPU && cam->model != RT_CAMERA_GPU) return RT_ERR_INVALID;
-  if (cam->model == RT_CAMERA_CPU && (prm->width < 2 || prm->height < 2)) return RT_ERR_INVALID;
-  if (!c->d_geom) return RT_ERR_NO_SCENE;
-  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+}  // extern "C"
+
+namespace {
+
+// rt_render_async's body.  ev_start (may be null) is recorded on the stream
+// just before the render kernel itself, after any one-time setup (the pilot,
+// buffer growth), so that rt_render's kernel_ms times the render alone.
+int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, float *accum_rgb, hipStream_t st,
+                   hipEvent_t ev_start) {
   RT_HIP(hipSetDevice(c->device));
+  // renders of one context are serialised, whatever streams they come on:
+  // they share the chunk and block-order scratch buffers
+  if (c->have_done && c->last_stream != st) RT_HIP(hipStreamWaitEvent(st, c->ev_done, 0));
   const uint64_t samples = (uint64_t)prm->width * (uint64_t)prm->local_rows * (uint64_t)prm->spp;
   if (prm->flags & RT_FLAG_KEEP_COUNTERS) {
     c->last_samples += samples;
@@ -1673,7 +1863,10 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
     c->last_samples = samples;
   }
   c->last_stats = (prm->flags & RT_FLAG_COUNT_WORK) != 0;
-  if (prm->width == 0 || prm->local_rows == 0) return RT_OK;
+  if (prm->width == 0 || prm->local_rows == 0) {
+    if (ev_start) RT_HIP(hipEventRecord(ev_start, st));
+    return RT_OK;
+  }
 
   rtk::kparams kp;
   std::memset(&kp, 0, sizeof kp);
@@ -1753,11 +1946,12 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
   if (units > 1) {
     const size_t need = (size_t)n_chunks * kp.chunk_stride;
     if (need > c->chunk_floats) {
-      RT_HIP(hipDeviceSynchronize());  // an earlier launch on any stream may still use it
-      (void)hipFree(c->d_chunks);
+      // stream-ordered: the old buffer is released after the renders already
+      // queued on st (and, through ev_done, on any other stream) have run
+      if (c->d_chunks) RT_HIP(hipFreeAsync(c->d_chunks, st));
       c->d_chunks = nullptr;
       c->chunk_floats = 0;
-      RT_HIP(hipMalloc(&c->d_chunks, need * sizeof(float)));
+      RT_HIP(hipMallocAsync((void **)&c->d_chunks, need * sizeof(float), st));
       c->chunk_floats = need;
     }
     chunks = c->d_chunks;
@@ -1770,48 +1964,46 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
     // units of a tile group adjacent.  Without it the hardware launches
     // blocks in index order and the last wave slots to fill may get the most
     // expensive tiles.  Scheduling only: the image does not depend on it.
+    // Everything stays on st (the sort runs on the device, rt_sched.hip).
     std::vector<uint64_t> key = {(uint64_t)prm->width, (uint64_t)prm->height, (uint64_t)prm->local_rows,
                                  (uint64_t)prm->row_block, (uint64_t)prm->band_stride,
                                  (uint64_t)prm->band_offset, (uint64_t)units, (uint64_t)(prm->flags & 0x12ffu)};
     const uint32_t *cw = reinterpret_cast<const uint32_t *>(cam);
     for (size_t k = 0; k < sizeof(rt_camera) / 4; ++k) key.push_back(cw[k]);
     if (key != c->order_key || c->order_n != (size_t)blocks * units) {
+      c->order_key.clear();  // valid again only once the new order is enqueued
       // tile costs, then 8 scratch counters (the context's are not touched)
       const size_t n_cost = (size_t)blocks * rtk::kWavesPerBlock;
       const size_t cost_bytes = (n_cost * sizeof(uint32_t) + 7) / 8 * 8;
       uint32_t *d_cost = nullptr;
-      RT_HIP(hipMalloc(&d_cost, cost_bytes + 8 * sizeof(unsigned long long)));
-      RT_HIP(hipMemsetAsync(d_cost, 0, cost_bytes + 8 * sizeof(unsigned long long), st));
-      rtk::kparams pk = kp;
-      pk.spp = std::min(prm->spp, 4);
-      pk.n_chunks = 1;
-      pk.units = 1;
-      pk.chunks_per_unit = 1;
-      pk.tile_cost = d_cost;
-      pk.counters = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(d_cost) + cost_bytes);
-      kLaunch[(v & 23) | 8](blocks, st, pk, c, accum_rgb, nullptr);
-      RT_HIP(hipGetLastError());
-      std::vector<uint32_t> cost((size_t)blocks * rtk::kWavesPerBlock);
-      RT_HIP(hipMemcpyAsync(cost.data(), d_cost, cost.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-      RT_HIP(hipStreamSynchronize(st));
-      (void)hipFree(d_cost);
-      std::vector<uint64_t> bc(blocks, 0);
-      for (size_t t = 0; t < cost.size(); ++t) bc[t / rtk::kWavesPerBlock] += cost[t];
-      std::vector<uint32_t> tb(blocks);
-      for (uint32_t b = 0; b < blocks; ++b) tb[b] = b;
-      std::stable_sort(tb.begin(), tb.end(), [&](uint32_t a, uint32_t b) { return bc[a] > bc[b]; });
-      std::vector<uint32_t> order((size_t)blocks * units);
-      for (size_t i = 0; i < tb.size(); ++i)
-        for (long long u = 0; u < units; ++u) order[i * units + u] = (uint32_t)(tb[i] * units + u);
-      (void)hipFree(c->d_order);
-      c->d_order = nullptr;
-      RT_HIP(hipMalloc(&c->d_order, order.size() * sizeof(uint32_t)));
-      RT_HIP(hipMemcpy(c->d_order, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-      c->order_n = order.size();
+      RT_HIP(hipMallocAsync((void **)&d_cost, cost_bytes + 8 * sizeof(unsigned long long), st));
+      hipError_t e = hipMemsetAsync(d_cost, 0, cost_bytes + 8 * sizeof(unsigned long long), st);
+      if (e == hipSuccess) {
+        rtk::kparams pk = kp;
+        pk.spp = std::min(prm->spp, 4);
+        pk.n_chunks = 1;
+        pk.units = 1;
+        pk.chunks_per_unit = 1;
+        pk.tile_cost = d_cost;
+        pk.counters = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(d_cost) + cost_bytes);
+        kLaunch[(v & 23) | 8](blocks, st, pk, c, accum_rgb, nullptr);
+        e = hipGetLastError();
+      }
+      if (e == hipSuccess && c->d_order) e = hipFreeAsync(c->d_order, st);
+      if (e == hipSuccess) {
+        c->d_order = nullptr;
+        c->order_n = 0;
+        e = hipMallocAsync((void **)&c->d_order, (size_t)blocks * units * sizeof(uint32_t), st);
+      }
+      if (e == hipSuccess) e = rt_internal_block_order(d_cost, blocks, (uint32_t)units, c->d_order, st);
+      (void)hipFreeAsync(d_cost, st);  // also on error: no leak
+      if (e != hipSuccess) return hip_fail(e);
+      c->order_n = (size_t)blocks * units;
       c->order_key = key;
     }
     kp.block_order = c->d_order;
   }
+  if (ev_start) RT_HIP(hipEventRecord(ev_start, st));
   kLaunch[v]((unsigned)(blocks * units), st, kp, c, accum_rgb, chunks);
   RT_HIP(hipGetLastError());
   if (units > 1) {
@@ -1821,7 +2013,24 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
                                            prm->row_block, prm->band_stride, prm->band_offset);
     RT_HIP(hipGetLastError());
   }
+  RT_HIP(hipEventRecord(c->ev_done, st));
+  c->last_stream = st;
+  c->have_done = true;
   return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, float *accum_rgb,
+                    void *stream) {
+  if (!c || !cam || !params_ok(prm) || (!accum_rgb && prm->local_rows && prm->width))
+    return RT_ERR_INVALID;
+  if (cam->model != RT_CAMERA_CPU && cam->model != RT_CAMERA_GPU) return RT_ERR_INVALID;
+  if (cam->model == RT_CAMERA_CPU && (prm->width < 2 || prm->height < 2)) return RT_ERR_INVALID;
+  if (!c->d_geom) return RT_ERR_NO_SCENE;
+  return render_enqueue(c, cam, prm, accum_rgb, stream ? (hipStream_t)stream : c->stream, nullptr);
 }
 
 int rt_reset_stats(rt_context *c, void *stream) {
@@ -1856,15 +2065,18 @@ int rt_render(rt_context *c, const rt_camera *cam, const rt_params *prm, float *
   const size_t nf = 3 * (size_t)prm->width * (size_t)prm->local_rows;
   RT_HIP(hipSetDevice(c->device));
   if (nf > c->frame_floats) {
+    // (only rt_render uses d_frame, and it returns after its work is done)
     (void)hipFree(c->d_frame);
-  (void)hipFree(c->d_chunks);
     c->d_frame = nullptr;
     c->frame_floats = 0;
     RT_HIP(hipMalloc(&c->d_frame, nf * sizeof(float)));
     c->frame_floats = nf;
   }
-  RT_HIP(hipEventRecord(c->ev0, c->stream));
-  int st = rt_render_async(c, cam, prm, c->d_frame, c->stream);
+  if (!cam || (cam->model != RT_CAMERA_CPU && cam->model != RT_CAMERA_GPU)) return RT_ERR_INVALID;
+  if (cam->model == RT_CAMERA_CPU && (prm->width < 2 || prm->height < 2)) return RT_ERR_INVALID;
+  if (!c->d_geom) return RT_ERR_NO_SCENE;
+  // ev0 is recorded right before the render kernel (after a first-frame pilot)
+  int st = render_enqueue(c, cam, prm, c->d_frame, c->stream, c->ev0);
   if (st != RT_OK) return st;
   RT_HIP(hipEventRecord(c->ev1, c->stream));
   RT_HIP(hipEventSynchronize(c->ev1));
@@ -1876,6 +2088,44 @@ int rt_render(rt_context *c, const rt_camera *cam, const rt_params *prm, float *
     if (st != RT_OK) return st;
     stats->kernel_ms = ms;
   }
+  return RT_OK;
+}
+
+int rt_device_kat(int device, int kind, const double *in, size_t n_cases, double *out) {
+  if (kind < RT_KAT_SPHERE_HIT || kind > RT_KAT_REFLECTANCE || (n_cases && (!in || !out)) ||
+      n_cases > (1u << 20))
+    return RT_ERR_INVALID;
+  if (!n_cases) return RT_OK;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return RT_ERR_NO_DEVICE;
+  RT_HIP(hipSetDevice(device));
+  double *d = nullptr;
+  RT_HIP(hipMalloc(&d, 19 * sizeof(double) * n_cases));
+  hipError_t e = hipMemcpy(d, in, 10 * sizeof(double) * n_cases, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    rtk::kat_kernel<<<(unsigned)((n_cases + 63) / 64), 64>>>(kind, d, (int)n_cases, d + 10 * n_cases);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(out, d + 10 * n_cases, 9 * sizeof(double) * n_cases, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return hip_fail(e);
+  return RT_OK;
+}
+
+int rt_tonemap_async(rt_context *c, const float *d_sums, size_t n_pixels, int spp, int mode, uint8_t *d_out,
+                     void *stream) {
+  if (!c || spp < 1 || (mode != RT_TONEMAP_CPU && mode != RT_TONEMAP_GPU) || ((!d_sums || !d_out) && n_pixels))
+    return RT_ERR_INVALID;
+  if (!n_pixels) return RT_OK;
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  RT_HIP(hipSetDevice(c->device));
+  const uint64_t n = 3 * (uint64_t)n_pixels;
+  const unsigned grid = (unsigned)std::min<uint64_t>((n / 4 + 255) / 256 + 1, 256u * 32u);
+  if (mode == RT_TONEMAP_CPU)
+    rtk::tonemap_kernel<false, double><<<grid, 256, 0, st>>>(d_sums, n, 1.0 / spp, c->d_thr64, d_out);
+  else
+    rtk::tonemap_kernel<true, float><<<grid, 256, 0, st>>>(d_sums, n, 1.0f / (float)spp, c->d_thr32, d_out);
+  RT_HIP(hipGetLastError());
   return RT_OK;
 }
 

@@ -34,6 +34,9 @@ RT_FLAG_COUNT_WORK = 1 << 10
 RT_FLAG_PILOT_SCHEDULE = 1 << 11  # launch expensive tiles first (4-spp pilot per frame geometry)
 RT_FLAG_LAYER_BVH = 1 << 12  # layer scenes: walk the layer BVH instead of the layer grid
 RT_CHUNK_SPP = 64  # include/rt.h: samples per chunk of the two-level pixel sum
+RT_TONEMAP_CPU, RT_TONEMAP_GPU = 0, 1  # write_color of src/cpu (fp64) / src/gpu (fp32)
+RT_KAT_SPHERE_HIT, RT_KAT_REFLECT, RT_KAT_REFRACT, RT_KAT_REFLECTANCE = 0, 1, 2, 3
+ABI_VERSION = 2
 
 _f = ctypes.POINTER(ctypes.c_float)
 _u32 = ctypes.POINTER(ctypes.c_uint32)
@@ -111,6 +114,12 @@ def lib():
         L.rt_collect_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(Stats)]
         L.rt_reset_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.rt_tonemap_u8.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+        L.rt_tonemap_u8_mode.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_void_p]
+        L.rt_tonemap_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.rt_device_kat.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                    ctypes.c_void_p]
         L.rt_write_ppm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_int]
         _lib = L
@@ -289,6 +298,11 @@ class Context:
                                     ctypes.c_void_p(dev_ptr), ctypes.c_void_p(stream)),
               "rt_render_async")
 
+    def tonemap_async(self, dev_sums, n_pixels, spp, dev_out, mode=RT_TONEMAP_CPU, stream=0):
+        """write_color on the device: fp32 sums -> bytes, both device pointers."""
+        check(lib().rt_tonemap_async(self._h, ctypes.c_void_p(dev_sums), n_pixels, spp, mode,
+                                     ctypes.c_void_p(dev_out), ctypes.c_void_p(stream)), "rt_tonemap_async")
+
     def reset_stats(self, stream=0):
         check(lib().rt_reset_stats(self._h, ctypes.c_void_p(stream)), "rt_reset_stats")
 
@@ -298,11 +312,24 @@ class Context:
         return st
 
 
-def tonemap(sums, spp):
+def tonemap(sums, spp, mode=RT_TONEMAP_CPU):
+    """write_color on the host: src/cpu's fp64 levels, or src/gpu's fp32 ones."""
     sums = np.ascontiguousarray(sums, dtype=np.float32)
     out = np.zeros(sums.shape, np.uint8)
     n_pix = sums.size // 3
-    check(lib().rt_tonemap_u8(sums.ctypes.data, n_pix, spp, out.ctypes.data), "rt_tonemap_u8")
+    check(lib().rt_tonemap_u8_mode(sums.ctypes.data, n_pix, spp, mode, out.ctypes.data),
+          "rt_tonemap_u8_mode")
+    return out
+
+
+def device_kat(kind, cases, device=0):
+    """Evaluate the render kernel's device arithmetic on known-answer cases
+    (rt_device_kat): cases [n, <=10] float64 -> [n, 9] float64."""
+    cases = np.asarray(cases, np.float64)
+    inp = np.zeros((cases.shape[0], 10), np.float64)
+    inp[:, :cases.shape[1]] = cases
+    out = np.zeros((cases.shape[0], 9), np.float64)
+    check(lib().rt_device_kat(device, kind, inp.ctypes.data, inp.shape[0], out.ctypes.data), "rt_device_kat")
     return out
 
 

@@ -10,11 +10,20 @@ oracle/_ref/ref_harness from the reference's own src/cpu sources
   ref_c0_shift_400x225x10.ppm.gz  same config, stream shifted by 10^7 draws
                              (the oracle's own stream-to-stream noise floor)
   ref_five_400x225x100.ppm.gz  five-sphere book scene (negative radius), 100 spp
+  ref_final_400x225x100(.|_shift).ppm.gz  final scene at 100 spp, and its
+                             stream-shifted twin (noise floor at 100 spp)
+  ref_five_dof_400x225x64(.|_shift).ppm.gz  five-sphere scene with image22's
+                             depth of field (defocus 10 deg at focus 3.4,
+                             archive-gpu/image22/camera.h:65-71: lens radius
+                             3.4 tan 5 deg, i.e. aperture 0.5949)
+  ref_tenk_160x90x16(.|_shift).ppm.gz  the 10 000-sphere stress scene
+                             (rt_scene_final(50), dumped to a temp file and
+                             rendered by the reference's own classes)
   ref_stats.json             segments / sphere tests / seconds per render + SHA-256
   kat.jsonl                  known-answer vectors: camera basis, sphere::hit,
                              reflect, refract, reflectance, write_color
 
-Usage: python tests/golden/make_golden.py
+Usage: python tests/golden/make_golden.py [--only NAME ...]
 """
 import gzip
 import hashlib
@@ -32,32 +41,76 @@ def run(args, **kw):
     return subprocess.run([HARNESS] + args, check=True, capture_output=True, **kw)
 
 
+def dump_scene(scene, path):
+    """The scene in ref_harness's `scene` format (float32 values printed exactly)."""
+    kinds = "LMD"
+    with open(path, "w") as f:
+        for i in range(scene.n):
+            a = scene.albedo[i]
+            f.write("%s %.9g %.9g %.9g %.9g %.9g %.9g %.9g %.9g\n" % (
+                kinds[int(scene.kind[i])], scene.cx[i], scene.cy[i], scene.cz[i], scene.radius[i],
+                a[0], a[1], a[2], scene.param[i]))
+
+
 def main():
+    import argparse
+    import math
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", default=None, help="render only these fixtures (stats are merged)")
+    a = ap.parse_args()
     if not os.path.isdir("/root/reference"):
         sys.exit("make_golden.py needs /root/reference (build container only)")
     subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
-    with open(os.path.join(HERE, "scene_final_gcc.txt"), "wb") as f:
-        f.write(run(["scene"]).stdout)
-    with open(os.path.join(HERE, "kat.jsonl"), "wb") as f:
-        f.write(run(["kat"]).stdout)
-    stats = {}
+    if a.only is None:
+        with open(os.path.join(HERE, "scene_final_gcc.txt"), "wb") as f:
+            f.write(run(["scene"]).stdout)
+        with open(os.path.join(HERE, "kat.jsonl"), "wb") as f:
+            f.write(run(["kat"]).stdout)
+    sys.path.insert(0, os.path.join(ROOT, "ray-tracing-in-one-weekend_amd"))
+    import rtow  # the product's host scene builder (no GPU needed)
+    tmp = tempfile.mkdtemp()
+    tenk = os.path.join(tmp, "tenk.txt")
+    dump_scene(rtow.final_scene(half_extent=50), tenk)
+    dof = "%.17g" % (2 * 3.4 * math.tan(math.radians(10.0 / 2)))
+    shift = "10000000"
     renders = {
         "ref_c0_400x225x10": ["render", "400", "16", "9", "10", "50", "final", "0"],
-        "ref_c0_shift_400x225x10": ["render", "400", "16", "9", "10", "50", "final", "10000000"],
+        "ref_c0_shift_400x225x10": ["render", "400", "16", "9", "10", "50", "final", shift],
         "ref_five_400x225x100": ["render", "400", "16", "9", "100", "50", "five", "0"],
+        "ref_final_400x225x100": ["render", "400", "16", "9", "100", "50", "final", "0"],
+        "ref_final_shift_400x225x100": ["render", "400", "16", "9", "100", "50", "final", shift],
+        "ref_five_dof_400x225x64": ["render", "400", "16", "9", "64", "50", "five", "0", dof, "3.4"],
+        "ref_five_dof_shift_400x225x64": ["render", "400", "16", "9", "64", "50", "five", shift, dof, "3.4"],
+        "ref_tenk_160x90x16": ["render", "160", "16", "9", "16", "50", "file:" + tenk, "0"],
+        "ref_tenk_shift_160x90x16": ["render", "160", "16", "9", "16", "50", "file:" + tenk, shift],
     }
-    for name, args in renders.items():
+    if a.only is not None:
+        renders = {k: v for k, v in renders.items() if k in a.only}
+    stats_path = os.path.join(HERE, "ref_stats.json")
+    stats = {}
+    if a.only is not None and os.path.exists(stats_path):
+        with open(stats_path) as f:
+            stats = json.load(f)
+
+    def one(item):
+        name, args = item
         r = run(args)
         ppm = r.stdout
         st = json.loads(r.stderr.decode().strip().splitlines()[-1])
         st["sha256"] = hashlib.sha256(ppm).hexdigest()
         st["bytes"] = len(ppm)
-        st["args"] = args
-        stats[name] = st
+        st["args"] = [x if not x.startswith("file:") else "file:<rt_scene_final(50) dump>" for x in args]
         with gzip.GzipFile(os.path.join(HERE, name + ".ppm.gz"), "wb", mtime=0) as g:
             g.write(ppm)
-        print(name, st)
-    with open(os.path.join(HERE, "ref_stats.json"), "w") as f:
+        print(name, st, flush=True)
+        return name, st
+
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        for name, st in ex.map(one, renders.items()):
+            stats[name] = st
+    with open(stats_path, "w") as f:
         json.dump(stats, f, indent=1, sort_keys=True)
 
 

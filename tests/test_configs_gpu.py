@@ -1,0 +1,198 @@
+"""GPU tests at the BASELINE.json configs (C1, C3, C4) and on the context's
+buffer lifecycle.
+
+  C1  1x MI355X, 1920x1080 @ 100 spp (the automatic chunk split: units = 2)
+  C3  8x MI355X, 7680x4320 @ 1000 spp: one rank's 1/8 band (world = 8), run
+      here on one GPU at reduced spp -- rank 0 and rank 7
+  C4  8x MI355X, 16384x16384, 10 000 spheres @ 2000 spp: rank 0's 1/8 band
+
+Each asserts the accelerated walk (layer grid, the bench default) equals the
+brute-force scan -- or the layer BVH where the scan is too slow -- bit for bit
+with equal segment counts, plus an 8-row slice checked against the oracle's
+kernel-mode restatement (the loop of /root/reference/src/cpu/main.cc:111-123).
+"""
+import numpy as np
+import pytest
+
+from oracle_lib import kernel_render
+
+pytestmark = pytest.mark.gpu
+
+GRID = 1 << 9                 # RT_FLAG_ACCEL_BVH: the layer grid on layer scenes
+LAYER_BVH = (1 << 9) | (1 << 12)
+
+
+def band_params(rtow, W, H, spp, world, rank, rows=None, **kw):
+    """Rank `rank`'s interleaved 8-row bands of a `world`-way split; rows=8
+    keeps only its first band (global rows rank*8 .. rank*8+7)."""
+    p = rtow.make_params(W, H, spp, rank=rank, world=world, row_block=8, **kw)
+    if rows is not None:
+        p.local_rows = rows
+    return p
+
+
+def same(a, sa, b, sb):
+    n_diff = int((a != b).sum())
+    assert n_diff == 0, f"{n_diff} floats differ"
+    assert sa.segments == sb.segments
+
+
+def test_c1_full_frame_100spp_grid_equals_scan(rtow, gpu_ctx):
+    """C1 at its own spp: 1920x1080 has 32 400 tiles, so the automatic units
+    splits every pixel's two chunks (64 + 36) over 2 waves; the grid walk and
+    the scan give the same sums, and so do units = 1 and the pilot schedule."""
+    gpu_ctx.upload(rtow.final_scene())
+    cam = rtow.camera_cpu(aspect=1920 / 1080)
+    p = rtow.make_params(1920, 1080, 100, seed=100)
+    a, sa = gpu_ctx.render(cam, p)
+    assert sa.samples == 1920 * 1080 * 100
+    for flags, units in ((GRID, 0), (GRID, 1), (GRID | rtow.RT_FLAG_PILOT_SCHEDULE, 0)):
+        q = rtow.make_params(1920, 1080, 100, seed=100, flags=flags, units=units)
+        b, sb = gpu_ctx.render(cam, q)
+        same(a, sa, b, sb)
+    assert np.isfinite(a).all() and a.max() <= 100 + 1e-3
+
+
+@pytest.mark.parametrize("rank", [0, 5])
+def test_c1_band_bit_exact_vs_oracle(rtow, gpu_ctx, oracle, rank):
+    """One 8-row band of C1 (rows rank*8.. of an 8-way split) at 100 spp,
+    chunks split over 2 waves: bit-exact vs the oracle on those rows."""
+    scene = rtow.final_scene()
+    gpu_ctx.upload(scene)
+    cam = rtow.camera_cpu(aspect=1920 / 1080)
+    p = band_params(rtow, 1920, 1080, 100, 8, rank, rows=8, seed=101, flags=GRID, units=2)
+    got, st = gpu_ctx.render(cam, p)
+    want, segs = kernel_render(scene, cam, p)
+    assert np.array_equal(got, want), int((got != want).sum())
+    assert st.segments == segs
+
+
+@pytest.mark.parametrize("rank", [0, 7])
+def test_c3_rank_share_grid_equals_scan(rtow, gpu_ctx, rank):
+    """C3 (7680x4320, 8 GPUs): rank 0's and rank 7's whole 1/8 share (540
+    rows in 8-row bands) at 130 spp (three chunks): the scan in one wave per
+    tile == the grid with the pilot schedule (automatic units) == the grid
+    with every tile's chunks split over 3 waves."""
+    gpu_ctx.upload(rtow.final_scene())
+    cam = rtow.camera_cpu(aspect=7680 / 4320)
+    p = band_params(rtow, 7680, 4320, 130, 8, rank, seed=300, units=1)
+    assert p.local_rows == 540
+    a, sa = gpu_ctx.render(cam, p)
+    assert sa.samples == 7680 * 540 * 130
+    for flags, units in ((GRID | rtow.RT_FLAG_PILOT_SCHEDULE, 0), (GRID, 3)):
+        q = band_params(rtow, 7680, 4320, 130, 8, rank, seed=300, flags=flags, units=units)
+        b, sb = gpu_ctx.render(cam, q)
+        same(a, sa, b, sb)
+
+
+@pytest.mark.parametrize("rank", [0, 7])
+def test_c3_band_bit_exact_vs_oracle(rtow, gpu_ctx, oracle, rank):
+    scene = rtow.final_scene()
+    gpu_ctx.upload(scene)
+    cam = rtow.camera_cpu(aspect=7680 / 4320)
+    p = band_params(rtow, 7680, 4320, 6, 8, rank, rows=8, seed=301, flags=GRID)
+    got, st = gpu_ctx.render(cam, p)
+    want, segs = kernel_render(scene, cam, p)
+    assert np.array_equal(got, want), int((got != want).sum())
+    assert st.segments == segs
+
+
+def test_c4_rank_share_grid_equals_layer_bvh_and_scan(rtow, gpu_ctx):
+    """C4 (16384x16384, 10 000 spheres, 8 GPUs): rank 0's whole 1/8 share
+    (2048 rows of 16384) at 2 spp: layer grid == layer BVH == brute-force scan
+    (10 004 tests per segment), on a scene whose grid has ~10 000 cells."""
+    scene = rtow.final_scene(half_extent=50)
+    assert 9900 < scene.n <= 10004
+    gpu_ctx.upload(scene)
+    cam = rtow.camera_cpu(aspect=1.0)
+    p = band_params(rtow, 16384, 16384, 2, 8, 0, seed=400, flags=GRID)
+    assert p.local_rows == 2048
+    a, sa = gpu_ctx.render(cam, p)
+    for flags in (LAYER_BVH, 0):
+        q = band_params(rtow, 16384, 16384, 2, 8, 0, seed=400, flags=flags)
+        b, sb = gpu_ctx.render(cam, q)
+        same(a, sa, b, sb)
+
+
+def test_c4_band_bit_exact_vs_oracle(rtow, gpu_ctx, oracle):
+    """One 8-row band of C4 (rank 3 of 8) at 1 spp, bit-exact vs the oracle's
+    brute-force restatement over all 10 004 spheres."""
+    scene = rtow.final_scene(half_extent=50)
+    gpu_ctx.upload(scene)
+    cam = rtow.camera_cpu(aspect=1.0)
+    p = band_params(rtow, 16384, 16384, 1, 8, 3, rows=8, seed=401, flags=GRID)
+    got, st = gpu_ctx.render(cam, p)
+    want, segs = kernel_render(scene, cam, p)
+    assert np.array_equal(got, want), int((got != want).sum())
+    assert st.segments == segs
+
+
+def test_chunk_buffer_survives_frame_growth(rtow):
+    """on one fresh context, a split-chunk render (units 2),
+    then a larger frame through rt_render (which grows the context's frame
+    buffer), then the first render again: the third image is bit-identical to
+    the first (the chunk buffer was neither freed nor reused by the frame),
+    and the context is destroyed cleanly."""
+    cam_s = rtow.camera_cpu(aspect=160 / 90)
+    cam_b = rtow.camera_cpu(aspect=3840 / 2160)
+    with rtow.Context(0) as ctx:
+        ctx.upload(rtow.final_scene())
+        p = rtow.make_params(160, 90, 100, seed=7, flags=GRID, units=2)
+        first, s1 = ctx.render(cam_s, p)
+        big, _ = ctx.render(cam_b, rtow.make_params(3840, 2160, 1, seed=8, flags=GRID))
+        third, s3 = ctx.render(cam_s, p)
+        assert np.array_equal(first, third) and s1.segments == s3.segments
+        # and a bigger split render after that (the chunk buffer grows)
+        q = rtow.make_params(640, 360, 130, seed=9, flags=GRID, units=3)
+        c, sc = ctx.render(rtow.camera_cpu(aspect=640 / 360), q)
+        q.units = 1
+        d, sd = ctx.render(rtow.camera_cpu(aspect=640 / 360), q)
+        assert np.array_equal(c, d) and sc.segments == sd.segments
+        again, _ = ctx.render(cam_s, p)
+        assert np.array_equal(first, again)
+
+
+def test_async_renders_on_two_streams_are_ordered(rtow):
+    """two split-chunk renders of one context enqueued on
+    two different streams share the chunk buffer; the context orders them
+    (the second waits for the first's event), so both images are right."""
+    import torch
+    with rtow.Context(0) as ctx:
+        ctx.upload(rtow.final_scene())
+        cam = rtow.camera_cpu(aspect=320 / 180)
+        pa = rtow.make_params(320, 180, 200, seed=11, flags=GRID, units=4)
+        pb = rtow.make_params(320, 180, 200, seed=12, flags=GRID, units=4)
+        want_a, _ = ctx.render(cam, pa)
+        want_b, _ = ctx.render(cam, pb)
+        dev = torch.device("cuda", 0)
+        s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        ta = torch.zeros((180, 320, 3), dtype=torch.float32, device=dev)
+        tb = torch.zeros_like(ta)
+        torch.cuda.synchronize(dev)
+        for _ in range(3):
+            ctx.render_async(cam, pa, ta.data_ptr(), s1.cuda_stream)
+            ctx.render_async(cam, pb, tb.data_ptr(), s2.cuda_stream)
+        torch.cuda.synchronize(dev)
+        assert np.array_equal(ta.cpu().numpy(), want_a)
+        assert np.array_equal(tb.cpu().numpy(), want_b)
+
+
+def test_pilot_first_render_is_asynchronous_and_correct(rtow):
+    """The pilot schedule's first render of a geometry enqueues the pilot, the
+    device sort and the render without a host sync; the result equals launch
+    order, and a different geometry afterwards gets its own order."""
+    import torch
+    with rtow.Context(0) as ctx:
+        ctx.upload(rtow.final_scene())
+        dev = torch.device("cuda", 0)
+        st = torch.cuda.Stream(dev)
+        for (w, h, spp, units) in ((640, 360, 80, 0), (200, 120, 130, 3)):
+            cam = rtow.camera_cpu(aspect=w / h)
+            want, _ = ctx.render(cam, rtow.make_params(w, h, spp, seed=5, flags=GRID, units=units))
+            t = torch.zeros((h, w, 3), dtype=torch.float32, device=dev)
+            torch.cuda.synchronize(dev)
+            p = rtow.make_params(w, h, spp, seed=5, flags=GRID | rtow.RT_FLAG_PILOT_SCHEDULE, units=units)
+            ctx.render_async(cam, p, t.data_ptr(), st.cuda_stream)
+            ctx.render_async(cam, p, t.data_ptr(), st.cuda_stream)  # cached order
+            torch.cuda.synchronize(dev)
+            assert np.array_equal(t.cpu().numpy(), want), (w, h)

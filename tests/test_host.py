@@ -91,6 +91,69 @@ def test_tonemap_matches_reference_formula(rtow):
     assert np.array_equal(got, want.astype(np.uint8))
 
 
+def test_tonemap_gpu_mode_matches_fp32_formula(rtow):
+    """RT_TONEMAP_GPU: src/gpu/color.h:16-38 in fp32 (scale = 1.0f/spp, sqrtf,
+    clamp to [0, 0.999f], int(256.0f * x))."""
+    rng = np.random.default_rng(1)
+    for spp in (1, 7, 10, 500, 2000):
+        sums = (rng.random((4000, 3)) * 1.2 * spp).astype(np.float32)
+        got = rtow.tonemap(sums, spp, rtow.RT_TONEMAP_GPU)
+        x = np.sqrt(sums * np.float32(np.float32(1.0) / np.float32(spp)))
+        x = np.clip(x, np.float32(0.0), np.float32(0.999))
+        want = (np.float32(256.0) * x).astype(np.int64)
+        assert np.array_equal(got, want.astype(np.uint8))
+
+
+def _level_edges(spp, fp32):
+    """Sums on both sides of every level boundary (k/256)^2 * spp, plus 0, NaN, inf."""
+    v = []
+    dt = np.float32 if fp32 else np.float64
+    for k in range(1, 256):
+        s = dt(k * k / 65536.0) * dt(spp)
+        f = np.float32(s)
+        v += [np.nextafter(f, np.float32(0)), f, np.nextafter(f, np.float32(np.inf))]
+    v += [0.0, np.nan, np.inf, 1e30]
+    v = np.array(v, np.float32)
+    return v[: len(v) // 3 * 3].reshape(-1, 3)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_tonemap_level_boundaries(rtow, mode):
+    """At every level boundary both modes follow their own arithmetic exactly;
+    the fp32 and fp64 levels differ somewhere (why src/gpu's mode exists)."""
+    for spp in (10, 100, 500):
+        sums = _level_edges(spp, mode == 1)
+        got = rtow.tonemap(sums, spp, mode)
+        if mode == 0:
+            x = np.sqrt(sums.astype(np.float64) * (1.0 / spp))
+            x = np.where(np.isnan(x), 0.0, np.clip(x, 0.0, 0.999))
+            want = (256 * x).astype(np.int64)
+        else:
+            with np.errstate(invalid="ignore"):
+                x = np.sqrt(sums * np.float32(np.float32(1.0) / np.float32(spp)))
+            x = np.where(np.isnan(x), np.float32(0), np.clip(x, np.float32(0.0), np.float32(0.999)))
+            want = (np.float32(256.0) * x).astype(np.int64)
+        assert np.array_equal(got, want.astype(np.uint8)), (spp, np.argwhere(got != want)[:5])
+    sums = _level_edges(10, True)
+    assert not np.array_equal(rtow.tonemap(sums, 10, 0), rtow.tonemap(sums, 10, 1))
+
+
+def test_ppm_writer_streams_large_frames(rtow, tmp_path):
+    """The threaded P3 writer (chunks of 65 536 pixels formatted by several
+    threads, written in order) gives exactly write_color's text."""
+    rng = np.random.default_rng(2)
+    img = rng.integers(0, 256, (1600, 1800, 3), dtype=np.uint8)
+    img[0, :5] = [[0, 0, 0], [255, 255, 255], [9, 10, 99], [100, 1, 0], [7, 77, 177]]
+    p3 = tmp_path / "big.ppm"
+    rtow.write_ppm(str(p3), img)
+    data = p3.read_bytes()
+    tab = [str(v).encode() for v in range(256)]
+    flat = img.reshape(-1, 3)
+    want = b"P3\n1800 1600\n255\n" + b"".join(
+        tab[r] + b" " + tab[g] + b" " + tab[b] + b"\n" for r, g, b in flat.tolist())
+    assert data == want
+
+
 def test_ppm_writer_p3_and_p6(rtow, tmp_path):
     ref = read_ppm_bytes(golden_ppm("ref_c0_400x225x10"))
     p3 = tmp_path / "a.ppm"
@@ -104,7 +167,7 @@ def test_ppm_writer_p3_and_p6(rtow, tmp_path):
 def test_abi_exports_every_declared_symbol(rtow):
     hdr = open(os.path.join(ROOT, "include", "rt.h")).read()
     names = sorted(set(re.findall(r"^\s*(?:[\w\*\s]+?)\b(rt_\w+)\s*\(", hdr, re.M)))
-    assert len(names) == 17, names
+    assert len(names) == 20, names
     L = rtow.lib()
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
@@ -119,7 +182,7 @@ def test_invalid_arguments_return_status(rtow):
     assert L.rt_scene_final(11, None, None) == -1
     assert L.rt_tonemap_u8(None, 4, 10, None) == -1
     assert L.rt_strerror(-4) == b"no such HIP device"
-    assert L.rt_abi_version() == 1
+    assert L.rt_abi_version() == rtow.ABI_VERSION == 2
     with pytest.raises(rtow.RTError):
         rtow.camera_cpu(aspect=0.0)
 
