@@ -149,7 +149,7 @@ typedef struct {
 
 typedef struct {
   uint64_t segments;     /* closest-hit queries (= hittable_list::hit calls) */
-  uint64_t samples;      /* primary samples rendered (width*rows*spp) */
+  uint64_t samples;      /* primary samples rendered (width * in-frame rows * spp) */
   uint64_t bf_tests;     /* brute-force equivalent ray-sphere tests: segments * spheres */
   uint64_t sphere_tests; /* executed lane-level ray-sphere tests (RT_FLAG_COUNT_WORK only) */
   uint64_t box_tests;    /* executed lane-level ray-box tests (RT_FLAG_COUNT_WORK only) */

@@ -1846,6 +1846,19 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
 
 namespace {
 
+// Local rows that lie inside the frame: a rank's last band slots may be
+// padding (global row >= height), which the kernel leaves at zero untraced.
+uint64_t valid_rows(const rt_params *prm) {
+  uint64_t n = 0;
+  for (int r0 = 0; r0 < prm->local_rows; r0 += prm->row_block) {
+    const long long g0 = ((long long)(r0 / prm->row_block) * prm->band_stride + prm->band_offset) *
+                         (long long)prm->row_block;
+    const long long in_band = std::min<long long>(prm->row_block, prm->local_rows - r0);
+    n += (uint64_t)std::max<long long>(0, std::min<long long>(in_band, prm->height - g0));
+  }
+  return n;
+}
+
 // rt_render_async's body.  ev_start (may be null) is recorded on the stream
 // just before the render kernel itself, after any one-time setup (the pilot,
 // buffer growth), so that rt_render's kernel_ms times the render alone.
@@ -1855,7 +1868,7 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
   // renders of one context are serialised, whatever streams they come on:
   // they share the chunk and block-order scratch buffers
   if (c->have_done && c->last_stream != st) RT_HIP(hipStreamWaitEvent(st, c->ev_done, 0));
-  const uint64_t samples = (uint64_t)prm->width * (uint64_t)prm->local_rows * (uint64_t)prm->spp;
+  const uint64_t samples = (uint64_t)prm->width * valid_rows(prm) * (uint64_t)prm->spp;
   if (prm->flags & RT_FLAG_KEEP_COUNTERS) {
     c->last_samples += samples;
   } else {

@@ -69,16 +69,21 @@ def test_c1_band_bit_exact_vs_oracle(rtow, gpu_ctx, oracle, rank):
 
 @pytest.mark.parametrize("rank", [0, 7])
 def test_c3_rank_share_grid_equals_scan(rtow, gpu_ctx, rank):
-    """C3 (7680x4320, 8 GPUs): rank 0's and rank 7's whole 1/8 share (540
-    rows in 8-row bands) at 130 spp (three chunks): the scan in one wave per
-    tile == the grid with the pilot schedule (automatic units) == the grid
-    with every tile's chunks split over 3 waves."""
+    """C3 (7680x4320, 8 GPUs): rank 0's and rank 7's whole 1/8 share (544
+    rows in 8-row bands, 536 of them inside the frame for ranks 4-7) at 130
+    spp (three chunks): the scan in one wave per tile == the grid with the
+    pilot schedule (automatic units) == the grid with every tile's chunks
+    split over 3 waves."""
     gpu_ctx.upload(rtow.final_scene())
     cam = rtow.camera_cpu(aspect=7680 / 4320)
     p = band_params(rtow, 7680, 4320, 130, 8, rank, seed=300, units=1)
-    assert p.local_rows == 540
+    # 540 bands of 8 rows over 8 ranks: every rank holds 68 band slots (544
+    # rows, padded so tiles are equal); rank 7's last slot lies past row 4319
+    assert p.local_rows == 544
+    valid = int((rtow.local_to_global_rows(p) < 4320).sum())
+    assert valid == (544 if rank < 4 else 536)
     a, sa = gpu_ctx.render(cam, p)
-    assert sa.samples == 7680 * 540 * 130
+    assert sa.samples == 7680 * valid * 130
     for flags, units in ((GRID | rtow.RT_FLAG_PILOT_SCHEDULE, 0), (GRID, 3)):
         q = band_params(rtow, 7680, 4320, 130, 8, rank, seed=300, flags=flags, units=units)
         b, sb = gpu_ctx.render(cam, q)
