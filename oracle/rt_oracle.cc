@@ -430,48 +430,43 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
       if (tr)
         std::fprintf(g_trace, "seg %d O=(%.9g %.9g %.9g) D=(%.9g %.9g %.9g) |O|^2=%.9g\n", depth, o[0],
                      o[1], o[2], d[0], d[1], d[2], o2);
-      for (size_t i = 0; i < n; ++i) {
-        const float h = fmaf_(sc.cz[i], d[2], fmaf_(sc.cx[i], d[0], fmaf_(sc.cy[i], d[1], nk1)));
-        const float g = fmaf_(sc.cz[i], oz2, fmaf_(sc.cx[i], ox2, fmaf_(sc.cy[i], oy2, o2)));
-        const float e = fmaf_(h, h, -g);
-        if (e >= sc.ks[i]) {
-          // sphere.h:34-44: the root offered is t0 if past t_min, else t1; it
-          // wins if closer than tmax (ties: last index for the closed src/cpu
-          // interval, first for the open src/gpu one -- what a sequential scan
-          // does, stated so that any visiting order gives the same winner)
-          const float sq = sqrt_k(e - sc.ks[i]);
-          const float t0 = h - sq, t1 = h + sq;
-          const bool use0 = k.open ? t0 > 0.001f : t0 >= 0.001f;
-          const float root = use0 ? t0 : t1;
-          const bool above = k.open ? root > 0.001f : root >= 0.001f;
-          const bool closer = root < tmax || (root == tmax && (k.open ? (long)i < best : (long)i > best));
-          if (tr)
-            std::fprintf(g_trace, "   cand %zu disc=%.9g t0=%.9g t1=%.9g root=%.9g above=%d closer=%d\n", i,
-                         e - sc.ks[i], t0, t1, root, (int)above, (int)closer);
-          if (above && closer) {
-            tmax = root;
-            near = use0;
-            best = (long)i;
+      auto closest = [&]() {
+        tmax = INFINITY;
+        best = -1;
+        near = true;
+        for (size_t i = 0; i < n; ++i) {
+          const float h = fmaf_(sc.cz[i], d[2], fmaf_(sc.cx[i], d[0], fmaf_(sc.cy[i], d[1], nk1)));
+          const float g = fmaf_(sc.cz[i], oz2, fmaf_(sc.cx[i], ox2, fmaf_(sc.cy[i], oy2, o2)));
+          const float e = fmaf_(h, h, -g);
+          if (e >= sc.ks[i]) {
+            // sphere.h:34-44: the root offered is t0 if past t_min, else t1; it
+            // wins if closer than tmax (ties: last index for the closed src/cpu
+            // interval, first for the open src/gpu one -- what a sequential scan
+            // does, stated so that any visiting order gives the same winner)
+            const float sq = sqrt_k(e - sc.ks[i]);
+            const float t0 = h - sq, t1 = h + sq;
+            const bool use0 = k.open ? t0 > 0.001f : t0 >= 0.001f;
+            const float root = use0 ? t0 : t1;
+            const bool above = k.open ? root > 0.001f : root >= 0.001f;
+            const bool closer = root < tmax || (root == tmax && (k.open ? (long)i < best : (long)i > best));
+            if (tr)
+              std::fprintf(g_trace, "   cand %zu disc=%.9g t0=%.9g t1=%.9g root=%.9g above=%d closer=%d\n", i,
+                           e - sc.ks[i], t0, t1, root, (int)above, (int)closer);
+            if (above && closer) {
+              tmax = root;
+              near = use0;
+              best = (long)i;
+            }
           }
         }
-      }
-      if (tr) std::fprintf(g_trace, "  -> best %ld t %.9g near %d\n", best, tmax, (int)near);
-      if (best < 0) {  // sky, main.cc:27-29
-        const float a = 0.5f * (d[1] + 1.0f);
-        const float s0 = 1.0f - a;
-        c[0] = fmaf_(th[0], fmaf_(a, 0.5f, s0), c[0]);
-        c[1] = fmaf_(th[1], fmaf_(a, 0.7f, s0), c[1]);
-        c[2] = fmaf_(th[2], s0 + a, c[2]);
-        break;
-      }
-      const size_t b = (size_t)best;
+      };
       // refine the winner's chosen root with the better-conditioned forms
-      // (DESIGN.md "Kernel algorithm", step 3)
-      float t = tmax;
-      {
+      // (DESIGN.md "Kernel algorithm", step 3); bb = (O - C).D
+      auto refine = [&](size_t b, float &bb) {
+        float t = tmax;
         const float r2 = sc.radius[b] * sc.radius[b];
         const float ocx = o[0] - sc.cx[b], ocy = o[1] - sc.cy[b], ocz = o[2] - sc.cz[b];
-        const float bb = dot3(ocx, ocy, ocz, d[0], d[1], d[2]);
+        bb = dot3(ocx, ocy, ocz, d[0], d[1], d[2]);
         float cc;
         if (r2 < o2 + std::fabs(sc.ks[b])) {
           cc = fmaf_(ocz, ocz, fmaf_(ocy, ocy, fmaf_(ocx, ocx, -r2)));
@@ -494,7 +489,38 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
           const float tr = near ? std::fmin(ta, tb) : std::fmax(ta, tb);
           if (std::isfinite(tr)) t = tr;
         }
+        return t;
+      };
+      closest();
+      float t = 0.0f;
+      if (best >= 0) {
+        float bb;
+        t = refine((size_t)best, bb);
+        // A refined root before t_min on a sphere the ray moves away from: the
+        // ray starts on that sphere and leaves its ball, which in exact
+        // arithmetic it cannot meet again (src/cpu, fp64, never does at
+        // t >= 0.001); the expanded quadratic's root was an fp32 artefact (for
+        // spheres far from the origin it can trap the path inside the
+        // sphere).  Not a segment: the ray moves on to the scan's root point
+        // (>= t_min further, so this ends) and walks again, same direction.
+        if (t < 0.001f && bb > 0.0f) {
+          if (tr) std::fprintf(g_trace, "  spurious best %ld t %.9g: skipped\n", best, tmax);
+          for (int a = 0; a < 3; ++a) o[a] = fmaf_(tmax, d[a], o[a]);
+          normalize3(d[0], d[1], d[2]);
+          --segs;
+          continue;
+        }
       }
+      if (tr) std::fprintf(g_trace, "  -> best %ld t %.9g near %d\n", best, tmax, (int)near);
+      if (best < 0) {  // sky, main.cc:27-29
+        const float a = 0.5f * (d[1] + 1.0f);
+        const float s0 = 1.0f - a;
+        c[0] = fmaf_(th[0], fmaf_(a, 0.5f, s0), c[0]);
+        c[1] = fmaf_(th[1], fmaf_(a, 0.7f, s0), c[1]);
+        c[2] = fmaf_(th[2], s0 + a, c[2]);
+        break;
+      }
+      const size_t b = (size_t)best;
       float p[3], nn[3];
       for (int a = 0; a < 3; ++a) p[a] = fmaf_(t, d[a], o[a]);
       nn[0] = (p[0] - sc.cx[b]) * sc.inv_r[b];

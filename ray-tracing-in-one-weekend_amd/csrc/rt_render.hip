@@ -390,6 +390,14 @@ __device__ __forceinline__ bool in_range(float t, float tmin, float tmax) {
   return (t >= tmin) & (t <= tmax);           // src/cpu/sphere.h:38-42
 }
 
+// This lane's index in its wave, recomputed where it is needed (volatile: not
+// hoisted, so it is not held in a VGPR through the bounce loop).
+__device__ __forceinline__ int lane_now() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
 // running closest hit of one lane (hittable_list::hit's closest_so_far/rec)
 struct hit_state {
   float tmax;
@@ -486,10 +494,12 @@ __device__ __forceinline__ void scan_pairs(const RT_CONST pair_geom *__restrict_
 //   roots q = -(b + sign(b) sqrt(disc)) and c / q  (no cancellation).
 __device__ __forceinline__ float refine_root(const shade_rec &sr, float t_scan, bool near,
                                              float ox, float oy, float oz, float dx, float dy,
-                                             float dz, float o2, float ox2, float oy2, float oz2) {
+                                             float dz, float o2, float ox2, float oy2, float oz2,
+                                             float &b_out) {
   const float r2 = sr.radius * sr.radius;
   const float ocx = ox - sr.cx, ocy = oy - sr.cy, ocz = oz - sr.cz;
   const float b = dot3(ocx, ocy, ocz, dx, dy, dz);
+  b_out = b;
   float c;
   if (r2 < o2 + fabsf(sr.ks)) {
     c = fmaf(ocz, ocz, fmaf(ocy, ocy, fmaf(ocx, ocx, -r2)));
@@ -551,14 +561,6 @@ __device__ __forceinline__ int walk_step(const bvh_node &nd, int node, bool hit,
   }
   if (LAYER) asm("v_min_f32 %0, %1, %2" : "=v"(lim) : "v"(lim_src), "v"(hs.tmax));
   return nd.skip;
-}
-
-// This lane's index in its wave, recomputed where it is needed (volatile: not
-// hoisted, so it is not held in a VGPR through the bounce loop).
-__device__ __forceinline__ int lane_now() {
-  int l;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-  return l;
 }
 
 // Per-lane 2-D DDA over the layer grid (layer mode): the lane visits the x-z
@@ -661,7 +663,8 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
   const bool scan_all = !BVH || __builtin_amdgcn_ballot_w64(o2 > p.oref2) != 0;
   if (scan_all) {
     // brute force: 8 spheres (4 pairs) per iteration over the whole array
-    for (int k = 0; k < n_pairs; k += 4) scan_pairs<OPEN, 4, STATS>(scan_geom + k, 2 * k, nullptr, rp, hs, wc.roots);
+    for (int k = 0; k < n_pairs; k += 4)
+      scan_pairs<OPEN, 4, STATS>(scan_geom + k, 2 * k, nullptr, rp, hs, wc.roots);
     if (STATS) wc.tests += 2 * n_pairs;
   } else {
     // wave-uniform stackless BVH walk: a node is entered if ANY lane's ray
@@ -847,7 +850,19 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         path_done = true;
       } else {
         const shade_rec sr = cload_g(as_global(q.shade) + best);
-        const float t = refine_root(sr, tmax, near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2);
+        float b;
+        const float t = refine_root(sr, tmax, near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2, b);
+        // A refined root before t_min on a sphere the ray moves away from
+        // (b > 0): the ray starts on that sphere and leaves its ball, which it
+        // cannot meet again; the expanded quadratic's root was an fp32 artefact
+        // (DESIGN.md 2, step 3).  Not a segment: the ray moves on to the
+        // scan's root point, same direction, and walks again.
+        if (t < 0.001f && b > 0.0f) {
+          ox = fmaf(tmax, dx, ox);
+          oy = fmaf(tmax, dy, oy);
+          oz = fmaf(tmax, dz, oz);
+          --segs;
+        } else {
         const float px = fmaf(t, dx, ox), py = fmaf(t, dy, oy), pz = fmaf(t, dz, oz);
         float nx = (px - sr.cx) * sr.inv_r, ny = (py - sr.cy) * sr.inv_r, nz = (pz - sr.cz) * sr.inv_r;
         // set_face_normal (hittable.h:16-19): dot(d, outward) < 0 is, in exact
@@ -913,6 +928,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           dx = sx;  // normalised below, with the new camera rays
           dy = sy;
           dz = sz;
+        }
         }
       }
       if (path_done) {
@@ -1058,7 +1074,8 @@ __global__ __launch_bounds__(64) void kat_kernel(int kind, const double *__restr
     hit_state hs{__builtin_huge_valf(), -1, 1};
     candidate<false>(e >= sr.ks, h, e - sr.ks, 0, hs);
     if (hs.best < 0) return;
-    const float t = refine_root(sr, hs.tmax, hs.near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2);
+    float b_unused;
+    const float t = refine_root(sr, hs.tmax, hs.near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2, b_unused);
     const float px = fmaf(t, dx, ox), py = fmaf(t, dy, oy), pz = fmaf(t, dz, oz);
     float nx = (px - sr.cx) * sr.inv_r, ny = (py - sr.cy) * sr.inv_r, nz = (pz - sr.cz) * sr.inv_r;
     const bool front = (hs.near != 0) != (sr.inv_r < 0.0f);

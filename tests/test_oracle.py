@@ -94,6 +94,28 @@ def test_kernel_algorithm_statistically_matches_reference_five_scene(rtow):
     assert blk < 1.5, blk
 
 
+@pytest.mark.slow
+def test_kernel_algorithm_matches_reference_ten_thousand_spheres(rtow):
+    """BASELINE C4's 10 000-sphere scene (coordinates up to 50): the fp32 kernel
+    algorithm does the reference's amount of work.  Without the spurious-root
+    rule the expanded quadratic's fp32 roots on spheres
+    far from the origin trapped paths inside them: +1.1 % segments, 119 paths
+    at the depth cap instead of 15 (profiles/r02_spurious_root.log)."""
+    scene = rtow.final_scene(half_extent=50)
+    cam = rtow.camera_cpu(aspect=16.0 / 9.0)
+    sums, segs = kernel_render(scene, cam, rtow.make_params(160, 90, 16, seed=777))
+    st = golden_stats()
+    ref_segs = st["ref_tenk_160x90x16"]["segments"]
+    floor = abs(st["ref_tenk_shift_160x90x16"]["segments"] / ref_segs - 1)  # 0.30 %
+    assert abs(segs / ref_segs - 1) < 2 * floor, (segs, ref_segs)
+    img = rtow.tonemap(sums, 16)
+    ref = read_ppm_bytes(golden_ppm("ref_tenk_160x90x16"))
+    ref2 = read_ppm_bytes(golden_ppm("ref_tenk_shift_160x90x16"))
+    bias, blk, floor_blk = stat_compare(img, ref, ref2)
+    assert np.all(np.abs(bias) <= 1.0), bias
+    assert blk <= 1.2 * floor_blk, (blk, floor_blk)
+
+
 def test_kernel_mode_partition_invariant(rtow):
     """RNG keyed by the global pixel: interleaved row bands over any rank count
     reassemble to the identical image."""

@@ -84,8 +84,13 @@ def test_ten_thousand_sphere_scene_vs_reference(rtow, gpu_ctx):
     sums, st = gpu_ctx.render(cam, rtow.make_params(160, 90, 16, seed=777, flags=GRID))
     img = device_tonemap(rtow, gpu_ctx, sums, 16)
     p2_compare(img, "ref_tenk_160x90x16")
-    ref_segs = golden_stats()["ref_tenk_160x90x16"]["segments"]
-    assert abs(st.segments / ref_segs - 1) < 0.01, (st.segments, ref_segs)
+    # the reference's own two streams differ by 0.30 % (625 108 vs 623 244);
+    # before the spurious-root rule fp32 self-hits on
+    # spheres far from the origin trapped paths: +1.1 %
+    stats = golden_stats()
+    ref_segs = stats["ref_tenk_160x90x16"]["segments"]
+    floor = abs(stats["ref_tenk_shift_160x90x16"]["segments"] / ref_segs - 1)
+    assert abs(st.segments / ref_segs - 1) < 2 * floor, (st.segments, ref_segs)
 
 
 def test_five_scene_depth_of_field_vs_reference(rtow, gpu_ctx):
