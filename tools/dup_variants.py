@@ -53,29 +53,54 @@ EDITS = {
       asm volatile("" : "+v"(pq));
       const uint4 r2 = pcg4d(pq, miss ? sample : sample - 1u, miss ? 0u : (uint32_t)(depth + 1), q.seed32);
         asm volatile("" :: "v"(r2.x), "v"(r2.y), "v"(r2.z));""")],
-    # sin/cos of the bounce's unit vector
-    "sincos": [("  sincos_turn(u2, s, c);\n  x = r * c;",
-                """  sincos_turn(u2, s, c);
-  float uu = u2, s2, c2;
+    # the per-step polar draw (sqrt + sin/cos)
+    "sincos": [("  sincos_turn(u, s, c);\n  x = rho * c;",
+                """  sincos_turn(u, s, c);
+  float uu = u, s2, c2;
   asm volatile("" : "+v"(uu));
   sincos_turn(uu, s2, c2);
   asm volatile("" :: "v"(s2), "v"(c2));
-  x = r * c;""")],
+  x = rho * c;""")],
     # the winner's root refinement
-    "refine": [("        const float t = refine_root(sr, tmax, near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2);",
-                """        const float t = refine_root(sr, tmax, near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2);
-        float tq = tmax;
+    "refine": [("        const float t = refine_root(sr, tmax, near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2, b);",
+                """        const float t = refine_root(sr, tmax, near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2, b);
+        float tq = tmax, b2;
         asm volatile("" : "+v"(tq));
-        const float t2 = refine_root(sr, tq, near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2);
-        asm volatile("" :: "v"(t2));""")],
-    # the camera ray of the next sample (path regeneration)
-    "camera": [("          camera_ray(k, rc, col, grow, ox, oy, oz, dx, dy, dz);",
-                """          camera_ray(k, rc, col, grow, ox, oy, oz, dx, dy, dz);
+        const float t2 = refine_root(sr, tq, near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2, b2);
+        asm volatile("" :: "v"(t2), "v"(b2));""")],
+    # the whole layer-grid walk (DDA + cell items + candidates), a second time
+    "gridwalk": [("        if (tyl_n <= tyl_fc) grid_walk<OPEN, STATS>(ox, oz, ix, iz, oix, oiz, tyl_n, tyl_fc, rg, hs, wc);",
+                  """        if (tyl_n <= tyl_fc) {
+          hit_state h2 = hs;
+          float ta2 = tyl_n;
+          asm volatile("" : "+v"(ta2), "+v"(h2.tmax));
+          grid_walk<OPEN, STATS>(ox, oz, ix, iz, oix, oiz, ta2, tyl_fc, rg, h2, wc);
+          asm volatile("" :: "v"(h2.tmax), "v"(h2.best), "v"(h2.near));
+        }
+        if (tyl_n <= tyl_fc) grid_walk<OPEN, STATS>(ox, oz, ix, iz, oix, oiz, tyl_n, tyl_fc, rg, hs, wc);""")],
+    # every candidate's root / interval sequence (sqrt, roots, tie rule)
+    "candidate": [("template <bool OPEN>\n__device__ __forceinline__ void candidate(bool c, float h, float disc, int idx, hit_state &hs) {\n  if (c) {",
+                   """template <bool OPEN>\n__device__ __forceinline__ void candidate(bool c, float h, float disc, int idx, hit_state &hs) {\n  if (c) {
+    {
+      float h2 = h, d2 = disc;
+      asm volatile("" : "+v"(h2), "+v"(d2));
+      const float sq2 = sqrt_k(d2);
+      const float a0 = h2 - sq2, a1 = h2 + sq2;
+      const bool u0 = OPEN ? (a0 > 0.001f) : (a0 >= 0.001f);
+      const float rt = u0 ? a0 : a1;
+      const bool ab = OPEN ? (rt > 0.001f) : (rt >= 0.001f);
+      const bool cl = (rt < hs.tmax) | ((rt == hs.tmax) & (OPEN ? (idx < hs.best) : (idx > hs.best)));
+      float o = (ab & cl) ? rt : 0.0f;
+      asm volatile("" :: "v"(o));
+    }""")],
+    # the camera direction of the next sample (path regeneration)
+    "camera": [("          camera_dir(k, rc, ddx, ddy, col, grow, ox, oy, oz, dx, dy, dz);",
+                """          camera_dir(k, rc, ddx, ddy, col, grow, ox, oy, oz, dx, dy, dz);
           {
             uint4 r2 = rc;
             asm volatile("" : "+v"(r2.x), "+v"(r2.y), "+v"(r2.z), "+v"(r2.w));
             float a0, a1, a2, a3, a4, a5;
-            camera_ray(k, r2, col, grow, a0, a1, a2, a3, a4, a5);
+            camera_dir(k, r2, ddx, ddy, col, grow, a0, a1, a2, a3, a4, a5);
             asm volatile("" :: "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5));
           }""")],
     # the material scatter (all three branches as the wave runs them)
@@ -96,12 +121,7 @@ def main():
         os.makedirs(d, exist_ok=True)
         p = os.path.join(d, "rt_render.hip")
         open(p, "w").write(s)
-        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
-                        "-ffp-contract=off", "-I" + os.path.join(ROOT, "include"),
-                        "-I" + os.path.join(ROOT, "ray-tracing-in-one-weekend_amd", "csrc"), "-shared",
-                        "-o", os.path.join(out, f"dup_{part}.so"), p,
-                        os.path.join(ROOT, "ray-tracing-in-one-weekend_amd", "csrc", "rt_host.cpp")],
-                       check=True)
+        subprocess.run([os.path.join(ROOT, "tools", "build_variant.sh"), "dup_" + part, p], check=True)
         print("built", f"dup_{part}.so")
 
 
