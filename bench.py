@@ -13,12 +13,18 @@ second of the max-over-ranks wall time / 1e6.
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
 Extra objects on the JSON line:
-  roofline     fp32 VALU roofline of the render kernel (algorithmic flops =
-               segments x spheres x 17 per launch / average launch time from
-               HIP events on the launch stream; peak 157.3 TFLOP/s)
+  roofline     fp32 VALU roofline of the render kernel: executed flops (ray-sphere
+               tests x 17 + grid cell steps x 2, counted in-kernel) per launch /
+               average launch time from HIP events on the launch stream, against
+               157.3 TFLOP/s; plus the VALU issue rate against the wave64 2-cycle
+               ceiling at the measured clock, HBM GB/s against 8 TB/s and the
+               VALU lane utilisation, from the committed rocprofv3 PMC summary
+               of the same kernel (profiles/pmc_traffic_bvh.json)
   cpu_baseline the reference's own src/cpu (oracle/_ref, built from
-               /root/reference sources) on 1 host core over a bounded sample,
-               falling back to the oracle's fp64 restatement (kind "port")
+               /root/reference sources) at C0 (400x225 @ 10 spp): one process
+               per host core (up to 16, the box's CPU share) rendering the same
+               frame, aggregate Mray/s; the 1-core figure beside it.  Falls back
+               to the oracle's fp64 restatement (kind "port")
 """
 import argparse
 import json
@@ -32,6 +38,9 @@ PKG = os.path.join(ROOT, "ray-tracing-in-one-weekend_amd")
 sys.path.insert(0, PKG)
 
 PEAK_FP32_TFLOPS = 157.3      # MI355X vector fp32 (MI355X_MICROARCH.md, chip table)
+PEAK_HBM_GBPS = 8000.0        # MI355X HBM3E (MI355X_MICROARCH.md)
+N_SIMD = 1024                 # 256 CUs x 4 SIMDs
+N_XCD = 8                     # GRBM_GUI_ACTIVE is summed over the 8 XCDs
 FLOPS_PER_TEST = 17           # algorithmic flops per ray-sphere test
 FLOPS_PER_BOX = 12            # slab test: 6 fma (2 flop) per ray-box test (layer BVH walk)
 FLOPS_PER_CELL = 2            # layer grid walk: one compare + one add per DDA cell step
@@ -69,7 +78,9 @@ def parse():
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl (= RCCL over xGMI); gloo only to rehearse the multi-process path "
                          "on a one-GPU box (tiles staged through host memory)")
-    ap.add_argument("--cpu-spp", type=int, default=30, help="spp of the bounded CPU sample (400x225)")
+    ap.add_argument("--cpu-spp", type=int, default=10, help="spp of the bounded CPU sample (400x225: C0)")
+    ap.add_argument("--cpu-procs", type=int, default=0,
+                    help="concurrent reference processes for the all-cores figure (0: min(16, cpu count))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pilot", action="store_true",
                     help="launch tiles in index order (no RT_FLAG_PILOT_SCHEDULE)")
@@ -80,25 +91,44 @@ def parse():
     return a
 
 
-def cpu_baseline(spp):
-    """Reference src/cpu (compiled from /root/reference by oracle/Makefile) on one
-    host core: 400x225 (C0 geometry) at `spp` samples, depth 50."""
-    sample = f"final scene 400x225 @ {spp} spp, depth 50, single thread"
+def _ref_run(harness, spp):
+    return subprocess.Popen([harness, "render", "400", "16", "9", str(spp), "50", "final", "0"],
+                            stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+
+
+def cpu_baseline(spp, procs):
+    """Reference src/cpu (compiled from /root/reference by oracle/Makefile) at C0
+    geometry (400x225, depth 50, `spp` samples): one process on one core, then
+    `procs` processes at once (the reference is single-threaded; its threaded
+    variant src/cpu-multi-threading is racy and out of scope), each
+    rendering the same frame: aggregate segments / wall time."""
+    sample = f"final scene 400x225 @ {spp} spp, depth 50 (C0)"
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     if os.path.exists(harness):
-        r = subprocess.run([harness, "render", "400", "16", "9", str(spp), "50", "final", "0"],
-                           stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, check=True, timeout=600)
-        st = json.loads(r.stderr.decode().strip().splitlines()[-1])
-        return {"value": round(st["segments"] / st["seconds"] / 1e6, 4), "unit": "Mray/s",
-                "cores": 1, "kind": "reference", "seconds": round(st["seconds"], 3),
-                "sample": sample + " (reference src/cpu, g++ -O2)"}
+        def run_many(n):
+            t = time.perf_counter()
+            ps = [_ref_run(harness, spp) for _ in range(n)]
+            segs = 0
+            for p in ps:
+                _, err = p.communicate(timeout=600)
+                if p.returncode != 0:
+                    raise RuntimeError(f"ref_harness exit {p.returncode}")
+                segs += json.loads(err.decode().strip().splitlines()[-1])["segments"]
+            return segs, time.perf_counter() - t
+        s1, t1 = run_many(1)
+        sn, tn = run_many(procs)
+        one = {"value": round(s1 / t1 / 1e6, 4), "cores": 1, "seconds": round(t1, 3)}
+        return {"value": round(sn / tn / 1e6, 4), "unit": "Mray/s", "cores": procs, "kind": "reference",
+                "seconds": round(tn, 3), "single_core": one,
+                "sample": f"{sample}: {procs} concurrent single-threaded processes of the reference "
+                          f"src/cpu (g++ -O2), aggregate; single_core = one process alone"}
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     t = time.perf_counter()
     _, segs = oracle_lib.reference_render(400, 16.0 / 9.0, spp)
     dt = time.perf_counter() - t
     return {"value": round(segs / dt / 1e6, 4), "unit": "Mray/s", "cores": 1, "kind": "port",
-            "seconds": round(dt, 3), "sample": sample + " (oracle fp64 restatement)"}
+            "seconds": round(dt, 3), "sample": sample + ", single thread (oracle fp64 restatement)"}
 
 
 def load_pmc(workload, accel="scan"):
@@ -110,6 +140,7 @@ def load_pmc(workload, accel="scan"):
         with open(path) as f:
             d = json.load(f)
         if d.get("workload") == workload:
+            d["path"] = path
             return d
     except (OSError, ValueError):
         pass
@@ -186,10 +217,20 @@ def main():
             dist.gather(tile if a.backend == "nccl" else tile.cpu(), gather_list, dst=0)
 
     assert stream.cuda_stream != 0
+    first_frame_ms = None
     with torch.cuda.stream(stream):
-        for i in range(a.warmup):
-            step(1000 + i)
+        # load the kernels (render + pilot builds) on a tiny frame, then time the
+        # first headline frame on its own: with the pilot schedule it includes
+        # the 4-spp pilot and the device sort of the tile order
+        small = rtow.make_params(64, 64, 4, flags=params.flags & ~rtow.RT_FLAG_KEEP_COUNTERS)
+        ctx.render_async(cam, small, tile.data_ptr(), stream.cuda_stream)
         torch.cuda.synchronize(dev)
+        for i in range(a.warmup):
+            t_first = time.perf_counter()
+            step(1000 + i)
+            torch.cuda.synchronize(dev)
+            if i == 0:
+                first_frame_ms = (time.perf_counter() - t_first) * 1e3
         ctx.reset_stats(stream.cuda_stream)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(a.steps)]
@@ -239,10 +280,31 @@ def main():
         flops = work.sphere_tests * FLOPS_PER_TEST + work.box_tests * (
             FLOPS_PER_CELL if a.accel == "bvh" else FLOPS_PER_BOX)
         achieved = flops / k_avg_s / 1e12
-        bf_achieved = work.bf_tests * FLOPS_PER_TEST / k_avg_s / 1e12
         value = segments / elapsed / 1e6
         pmc = load_pmc(workload, a.accel)
         valu_insts = pmc.get("valu_insts_per_launch")
+        cnt = pmc.get("counters_avg_per_dispatch", {})
+        traffic = pmc.get("hbm_bytes_per_launch")
+        clock_ghz = (cnt["GRBM_GUI_ACTIVE"] / N_XCD / k_avg_s / 1e9) if cnt.get("GRBM_GUI_ACTIVE") else None
+        valu_issue = None
+        if valu_insts:
+            rate = valu_insts / k_avg_s
+            valu_issue = {"achieved": round(rate / 1e9, 1), "unit": "G wave-instr/s",
+                          "source": "SQ_INSTS_VALU per launch (committed PMC summary) / this run's kernel time"}
+            if clock_ghz:
+                peak2 = N_SIMD * clock_ghz * 1e9 / 2  # one wave64 VALU instruction per 2 cycles per SIMD
+                valu_issue.update({"peak": round(peak2 / 1e9, 1), "frac": round(rate / peak2, 3),
+                                   "clock_ghz": round(clock_ghz, 3),
+                                   "peak_basis": "wave64 VALU issue every 2 cycles per SIMD "
+                                                 "(MI355X_MICROARCH.md) x 1024 SIMDs at the clock from "
+                                                 "GRBM_GUI_ACTIVE / 8 XCDs / kernel time"})
+            valu_issue.update({"peak_ubench": round(VALU_ISSUE_PEAK / 1e9, 1),
+                               "frac_ubench": round(rate / VALU_ISSUE_PEAK, 3),
+                               "peak_ubench_basis": "dependency-free v_fma_f32 stream, 1.041 ns per "
+                                                    "wave instruction per SIMD (tools/ubench_exec.hip)"})
+        lane_util = None
+        if cnt.get("SQ_THREAD_CYCLES_VALU") and cnt.get("SQ_ACTIVE_INST_VALU"):
+            lane_util = round(cnt["SQ_THREAD_CYCLES_VALU"] / (64.0 * cnt["SQ_ACTIVE_INST_VALU"]), 3)
         out = {
             "metric": "Mray/s (ray segments = closest-hit queries per second), final random-spheres "
                       "scene 3840x2160 @ 500spp depth 50" if not a.preset or a.preset == "c2"
@@ -277,26 +339,38 @@ def main():
             "work_per_launch_rank0": {"segments": work.segments, "sphere_tests": work.sphere_tests,
                                       "box_tests": work.box_tests, "box_hits_own_ray": work.box_hits,
                                       "brute_force_equiv_tests": work.bf_tests},
+            "first_frame_ms": round(first_frame_ms, 3) if first_frame_ms is not None else None,
+            "first_frame_note": "wall time of the first frame of this geometry on its own, pilot schedule "
+                                "included (4-spp pilot + device sort of the tile order); ms_per_step "
+                                "reuses the order",
             "roofline": {"bound": "valu", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                         "traffic": pmc.get("hbm_bytes_per_launch"),
-                         "brute_force_equiv_achieved": round(bf_achieved, 2),
-                         "valu_issue": ({"achieved": round(valu_insts / k_avg_s / 1e9, 1),
-                                         "peak": round(VALU_ISSUE_PEAK / 1e9, 1),
-                                         "unit": "G wave-instr/s",
-                                         "frac": round(valu_insts / k_avg_s / VALU_ISSUE_PEAK, 3),
-                                         "source": "SQ_INSTS_VALU per launch from the committed PMC "
-                                                   "summary / this run's kernel time"}
-                                        if valu_insts else None),
-                         "note": "fp32 VALU-bound (no MFMA): executed ray-sphere tests x 17 flop "
-                                 "+ grid cell steps x 2 flop (layer BVH: box tests x 12) per "
-                                 "launch / HIP-event kernel time; "
-                                 "the kernel is control-heavy (min/max, compares, branches), so "
-                                 "valu_issue is the bound it actually runs against"},
+                         "traffic": traffic,
+                         "achieved_basis": "executed work per launch (RT_FLAG_COUNT_WORK frame): "
+                                           "ray-sphere tests x 17 flop + grid cell steps x 2 flop "
+                                           "(layer BVH: box tests x 12) / HIP-event kernel time",
+                         "valu_issue": valu_issue,
+                         "valu_lane_util": lane_util,
+                         "valu_lane_util_basis": "SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU): "
+                                                 "mean active lanes per VALU instruction / 64",
+                         "hbm": ({"achieved_GBps": round(traffic / k_avg_s / 1e9, 1),
+                                  "peak_GBps": PEAK_HBM_GBPS,
+                                  "frac": round(traffic / k_avg_s / 1e9 / PEAK_HBM_GBPS, 5)}
+                                 if traffic else None),
+                         "pmc_source": os.path.relpath(pmc["path"], ROOT) if pmc.get("path") else None,
+                         "culling_speedup": round(work.bf_tests / max(1, work.sphere_tests), 1),
+                         "culling_speedup_basis": "brute-force ray-sphere tests (segments x spheres, "
+                                                  "SURVEY 8d) / tests the walk executes; not a roofline "
+                                                  "fraction",
+                         "note": "fp32 VALU-bound (no MFMA, HBM idle): the kernel is control-heavy "
+                                 "(compares, selects, branches, divergent per-lane walks), so "
+                                 "valu_issue and valu_lane_util say how close it runs to the issue "
+                                 "ceiling; frac counts only the algorithmic flops"},
         }
         if world == 1 and not a.no_cpu_baseline:
             try:
-                out["cpu_baseline"] = cpu_baseline(a.cpu_spp)
+                procs = a.cpu_procs or min(16, os.cpu_count() or 1)
+                out["cpu_baseline"] = cpu_baseline(a.cpu_spp, procs)
             except Exception as e:  # the GPU number stands on its own
                 out["cpu_baseline"] = {"value": None, "error": repr(e)[:200]}
         print(json.dumps(out), flush=True)

@@ -1,0 +1,103 @@
+"""The multi-process path on the GPU, rehearsed on a one-GPU box.
+
+Two ranks share cuda:0 and talk over gloo (RCCL does not put two ranks on
+one device); each renders its interleaved row bands with the HIP kernel
+through the C ABI and rank 0 gathers and de-interleaves the tiles.  The
+assembled frame must equal the single-rank frame bit for bit: the RNG is
+keyed by the global pixel, so the image does not depend on the rank count.
+The second test drives bench.py itself the way the driver does for N > 1
+(torch.distributed.run, one process per rank) and checks that it traces the
+same work as one rank.  On an 8-GPU node the driver runs
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \\
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus 8
+(backend nccl = RCCL over xGMI).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+W, H, SPP, SEED = 320, 181, 70, 5  # ragged height, two sample chunks
+GRID = 1 << 9
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, outdir):
+    import torch
+    import torch.distributed as dist
+    for p in (os.path.join(ROOT, "ray-tracing-in-one-weekend_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import rtow
+    import rtow_dist
+    ctx = rtow.Context(0)
+    ctx.upload(rtow.final_scene())
+    cam = rtow.camera_cpu(aspect=W / H)
+
+    def render_tile(p):
+        p.flags |= GRID | rtow.RT_FLAG_PILOT_SCHEDULE
+        out, st = ctx.render(cam, p)
+        np.save(os.path.join(outdir, f"segs_{rank}.npy"), np.array([st.segments], np.uint64))
+        return torch.from_numpy(out)
+
+    frame = rtow_dist.render_distributed(render_tile, W, H, SPP, world, rank, seed=SEED)
+    if rank == 0:
+        np.save(os.path.join(outdir, "frame.npy"), frame)
+    dist.barrier()
+    dist.destroy_process_group()
+    ctx.close()
+
+
+def test_two_ranks_on_gloo_equal_one_rank_bit_for_bit(rtow, gpu_ctx, tmp_path):
+    import torch.multiprocessing as mp
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    got = np.load(tmp_path / "frame.npy")
+    gpu_ctx.upload(rtow.final_scene())
+    want, st = gpu_ctx.render(rtow.camera_cpu(aspect=W / H), rtow.make_params(W, H, SPP, seed=SEED, flags=GRID))
+    assert got.shape == (H, W, 3)
+    assert np.array_equal(got, want)
+    segs = sum(int(np.load(tmp_path / f"segs_{r}.npy")[0]) for r in range(2))
+    assert segs == st.segments
+
+
+def _bench(args, nproc=1):
+    cmd = [sys.executable]
+    if nproc > 1:
+        cmd += ["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+                "--master-addr", "127.0.0.1", f"--master-port={_free_port()}"]
+    cmd += [os.path.join(ROOT, "bench.py")] + args
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    return json.loads(line)
+
+
+def test_bench_two_ranks_gloo_traces_the_same_frames():
+    """bench.py --gpus 2 (gloo rehearsal) renders the same frames as --gpus 1:
+    identical segment totals, both ranks' work counted, gather included."""
+    common = ["--steps", "2", "--warmup", "1", "--width", "256", "--height", "144", "--spp", "16",
+              "--no-cpu-baseline"]
+    one = _bench(common)
+    two = _bench(common + ["--gpus", "2", "--backend", "gloo"], nproc=2)
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    assert two["segments_per_frame"] == one["segments_per_frame"]
+    assert "gloo gather" in two["config"]["parallelism"]
+    assert two["value"] > 0 and one["first_frame_ms"] > 0

@@ -28,17 +28,30 @@ def main():
     ap.add_argument("--workload", default="")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
-    vals = defaultdict(list)
+    # only the full-size dispatches of the kernel: the bench also launches it on
+    # a tiny frame to load the code (and the pilot / work-count builds are
+    # other kernels), which must not enter the per-launch averages
+    rows = []
     for d in a.dirs:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             with open(f) as fh:
-                for row in csv.DictReader(fh):
-                    if a.kernel not in row.get("Kernel_Name", ""):
-                        continue
-                    vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+                rows += [r for r in csv.DictReader(fh) if a.kernel in r.get("Kernel_Name", "")]
+    grid = max((int(r["Grid_Size"]) for r in rows), default=0)
+    vals = defaultdict(list)
+    dur = {}
+    for r in rows:
+        if int(r["Grid_Size"]) != grid:
+            continue
+        vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        if r.get("Start_Timestamp") and r.get("End_Timestamp"):
+            dur[(r["Counter_Name"], r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
     avg = {k: sum(v) / len(v) for k, v in vals.items()}
-    out = {"kernel": a.kernel, "workload": a.workload, "counters_avg_per_dispatch": avg,
+    out = {"kernel": a.kernel, "workload": a.workload, "grid_size": grid, "counters_avg_per_dispatch": avg,
            "dispatches": {k: len(v) for k, v in vals.items()}}
+    g = [dur[k] for k in dur if k[0] == "GRBM_GUI_ACTIVE"]
+    if "GRBM_GUI_ACTIVE" in avg and g:
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs
+        out["clock_ghz_pmc_pass"] = round(avg["GRBM_GUI_ACTIVE"] / 8 / (sum(g) / len(g)) / 1e9, 3)
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         out["fetch_bytes"] = avg["FETCH_SIZE"] * 1024
         out["write_bytes"] = avg["WRITE_SIZE"] * 1024
