@@ -78,6 +78,24 @@ EDITS = {
           asm volatile("" :: "v"(h2.tmax), "v"(h2.best), "v"(h2.near));
         }
         if (tyl_n <= tyl_fc) grid_walk<OPEN, STATS>(ox, oz, ix, iz, oix, oiz, tyl_n, tyl_fc, rg, hs, wc);""")],
+    # the grid walk's item loads (16 B per lane from L1)
+    "itemload": [("      const f4 it = items[first + k];",
+                  """      const f4 it = items[first + k];
+      {
+        uint32_t kk = first + k;
+        asm volatile("" : "+v"(kk));
+        const f4 it2 = items[kk];
+        asm volatile("" :: "v"(it2.x), "v"(it2.y), "v"(it2.z), "v"(it2.w));
+      }""")],
+    # the grid walk's cell loads (4 B per lane)
+    "cellload": [("    const uint32_t ce = cells[(uint32_t)cell];",
+                  """    const uint32_t ce = cells[(uint32_t)cell];
+    {
+      uint32_t c2 = (uint32_t)cell;
+      asm volatile("" : "+v"(c2));
+      const uint32_t ce2 = cells[c2];
+      asm volatile("" :: "v"(ce2));
+    }""")],
     # every candidate's root / interval sequence (sqrt, roots, tie rule)
     "candidate": [("template <bool OPEN>\n__device__ __forceinline__ void candidate(bool c, float h, float disc, int idx, hit_state &hs) {\n  if (c) {",
                    """template <bool OPEN>\n__device__ __forceinline__ void candidate(bool c, float h, float disc, int idx, hit_state &hs) {\n  if (c) {
