@@ -151,7 +151,20 @@ struct kparams {
   float grid_xi, grid_zi;  // inner box (the listed region): [xi, x1] x [zi, z1]
   float grid_x1, grid_z1, grid_g, grid_invg;
   int grid_nx, grid_nz;    // cells including the ring
+  // LDS-resident grid (render_kernel<..., GLDS>): the block copies the items
+  // (16 B) and then the cells (as u16: first << 4 | count, first < 4096) into
+  // dynamic LDS at launch
+  int grid_n_items, grid_n_cells;
 };
+
+// the dynamic LDS of the GLDS builds: grid items, then the u16 cells
+extern __shared__ f4 s_grid_dyn[];
+__host__ __device__ constexpr size_t grid_lds_bytes(int n_items, int n_cells) {
+  return (size_t)n_items * 16u + ((size_t)n_cells * 2u + 15u) / 16u * 16u;
+}
+// LDS budget of the grid copy: 3 KB of static LDS + this stays within 20 KB
+// per 256-thread block, so 8 blocks (8 waves per SIMD) still fit in 160 KB
+constexpr size_t kGridLdsMax = 17 * 1024;
 
 // The kernel arguments, re-read from the kernarg segment (constant address
 // space: scalar loads that hit the scalar cache) at the rare places that need
@@ -572,7 +585,7 @@ __device__ __forceinline__ int walk_step(const bvh_node &nd, int node, bool hit,
 // cell (bvh_builder::build_grid), so the fp32 DDA's boundary errors cannot
 // skip a sphere that could win.  Lanes walk independently: the wave runs
 // until its last lane is done.
-template <bool OPEN, bool STATS>
+template <bool OPEN, bool STATS, bool GLDS>
 __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz, float oix, float oiz,
                                           float ta, float tb, const ray_pre &rl, hit_state &hs,
                                           work_ctr &wc) {
@@ -595,14 +608,17 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
   float tmx = fmaf(fmaf((float)(cx + (nxs ? 0 : 1)), p.grid_g, p.grid_x0), ix, oix);
   float tmz = fmaf(fmaf((float)(cz + (nzs ? 0 : 1)), p.grid_g, p.grid_z0), iz, oiz);
   const float tdx = p.grid_g * fabsf(ix), tdz = p.grid_g * fabsf(iz);
+  // GLDS: items and cells in LDS (ds_read: shorter latency than the L1 path
+  // and off the texture pipeline; 166 -> 157 ms)
   const RT_GLOBAL uint32_t *__restrict__ cells = as_global(p.grid_cells);
   const RT_GLOBAL f4 *__restrict__ items = as_global(p.grid_items);
+  const uint16_t *__restrict__ lcells = reinterpret_cast<const uint16_t *>(s_grid_dyn + p.grid_n_items);
   // The walk stops on time alone: it leaves the inner box only at t ~ tb and
   // the next boundary is a whole cell further, so it never steps past the ring.
   int cell = cz * nx + cx;
   const int dcx = nxs ? -1 : 1, dcz = nzs ? -nx : nx;
   while (true) {
-    const uint32_t ce = cells[(uint32_t)cell];
+    const uint32_t ce = GLDS ? (uint32_t)lcells[(uint32_t)cell] : cells[(uint32_t)cell];
     const uint32_t first = ce >> 4, cnt = ce & 15u;
     // STATS: boxes = lane-level cell visits; box_hits / roots = wave-level DDA
     // / item iterations (counted once per wave, by its first active lane)
@@ -612,7 +628,7 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
     }
     for (uint32_t k = 0; k < cnt; ++k) {
       if (STATS && RT_COUNT_ITEMS == 1 && lane_now() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true))) ++wc.box_hits;
-      const f4 it = items[first + k];
+      const f4 it = GLDS ? s_grid_dyn[first + k] : items[first + k];
       const float h = fmaf(it.y, dz, fmaf(it.x, dx, rl.nk1.x));
       const float g = fmaf(it.y, rl.oz2.x, fmaf(it.x, rl.ox2.x, rl.o2.x));
       const float e = fmaf(h, h, -g);
@@ -643,7 +659,7 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
 // The scene parameters are re-read from the kernarg segment on entry
 // (kernargs()): they live in SGPRs for the walk only, not across the whole
 // bounce loop (SGPR pressure).
-template <bool OPEN, bool BVH, bool STATS, bool GRID>
+template <bool OPEN, bool BVH, bool STATS, bool GRID, bool GLDS>
 __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, float dx, float dy, float dz,
                                                  work_ctr &wc) {
   const kparams p = kernargs();
@@ -709,7 +725,7 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
         ray_pre rg = rp;
         rg.nk1 = fma2(f2{p.layer_cy, p.layer_cy}, rp.dy, rp.nk1);
         rg.o2 = fma2(f2{p.layer_cy, p.layer_cy}, rp.oy2, rp.o2);
-        if (tyl_n <= tyl_fc) grid_walk<OPEN, STATS>(ox, oz, ix, iz, oix, oiz, tyl_n, tyl_fc, rg, hs, wc);
+        if (tyl_n <= tyl_fc) grid_walk<OPEN, STATS, GLDS>(ox, oz, ix, iz, oix, oiz, tyl_n, tyl_fc, rg, hs, wc);
         return hs;
       }
       // a wave none of whose rays crosses the layer before tmax skips the walk
@@ -763,7 +779,7 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
 // the kernarg segment where they are used (kernargs(), as_const()) instead of
 // being held in SGPRs for the whole kernel: 94 SGPRs + 21 spilled -> 69 at 7
 // waves.
-template <bool OPEN, bool METAL_UNIT, bool BVH, bool STATS, bool GRID>
+template <bool OPEN, bool METAL_UNIT, bool BVH, bool STATS, bool GRID, bool GLDS>
 __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   // Per-lane values that the bounce loop rarely needs are not kept live (VGPR
   // pressure at 8 waves): the wave keeps its tile origin (col0, lrow0, SGPRs)
@@ -800,6 +816,14 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   // fold_chunks
   __shared__ float s_tot[3][kBlock];
   s_tot[0][threadIdx.x] = s_tot[1][threadIdx.x] = s_tot[2][threadIdx.x] = 0.0f;
+  if (GLDS) {  // the block's copy of the layer grid (kparams grid_n_items)
+    const RT_GLOBAL f4 *gi = as_global(p.grid_items);
+    for (int i = (int)threadIdx.x; i < p.grid_n_items; i += kBlock) s_grid_dyn[i] = gi[i];
+    uint16_t *sc = reinterpret_cast<uint16_t *>(s_grid_dyn + p.grid_n_items);
+    const RT_GLOBAL uint32_t *gc = as_global(p.grid_cells);
+    for (int i = (int)threadIdx.x; i < p.grid_n_cells; i += kBlock) sc[i] = (uint16_t)gc[i];
+    __syncthreads();
+  }
   // (col, global row) of this lane's pixel from pix: col from the tile origin,
   // row by exact division (pix - col) / W
   auto pixel_cr = [&](const kparams &k, int &col, int &grow) {
@@ -817,7 +841,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   while (true) {
     hit_state hs{__builtin_huge_valf(), -1, 1};
     if (!__ballot(alive)) break;
-    if (alive) hs = closest_hit<OPEN, BVH, STATS, GRID>(ox, oy, oz, dx, dy, dz, wc);
+    if (alive) hs = closest_hit<OPEN, BVH, STATS, GRID, GLDS>(ox, oy, oz, dx, dy, dz, wc);
     ++steps;
     if (alive) {
       ++segs;
@@ -1172,6 +1196,8 @@ struct rt_context {
   uint32_t extra_pair0 = 0, n_extra_pairs = 0;
   uint32_t *d_grid_cells = nullptr;  // layer grid (nullptr: none)
   float *d_grid_items = nullptr;
+  size_t grid_n_items = 0;
+  bool grid_lds = false;  // the grid fits the LDS budget (render_kernel GLDS builds)
   float grid_x0 = 0, grid_z0 = 0, grid_xi = 0, grid_zi = 0, grid_x1 = 0, grid_z1 = 0, grid_g = 0;
   int grid_nx = 0, grid_nz = 0;
   unsigned long long *d_counters = nullptr;
@@ -1644,7 +1670,7 @@ void fill_slot(rtk::pair_geom &g, int l, const rt_scene_view *s, int i) {
   }
 }
 
-template <bool O, bool U, bool B, bool S, bool G = false>
+template <bool O, bool U, bool B, bool S, bool G = false, bool L = false>
 void launch(unsigned blocks, hipStream_t st, const rtk::kparams &kp0, rt_context *c, float *out, float *chunks) {
   rtk::kparams kp = kp0;
   kp.scan_geom = c->d_geom;
@@ -1655,30 +1681,26 @@ void launch(unsigned blocks, hipStream_t st, const rtk::kparams &kp0, rt_context
   kp.out = out;
   kp.chunks = chunks;
   if (!kp.counters) kp.counters = c->d_counters;  // (the pilot brings its own)
-  rtk::render_kernel<O, U, B, S, G><<<blocks, rtk::kBlock, 0, st>>>(kp);
+  const size_t lds = L ? rtk::grid_lds_bytes(kp.grid_n_items, kp.grid_n_cells) : 0u;
+  rtk::render_kernel<O, U, B, S, G, L><<<blocks, rtk::kBlock, lds, st>>>(kp);
 }
 
 using launch_fn = void (*)(unsigned, hipStream_t, const rtk::kparams &, rt_context *, float *, float *);
-// index: open | unit<<1 | bvh<<2 | stats<<3 | grid<<4 (grid: the layer grid
-// walk, a build of its own; without bvh the grid bit selects the scan)
-const launch_fn kLaunch[32] = {
-    launch<false, false, false, false>, launch<true, false, false, false>,
-    launch<false, true, false, false>,  launch<true, true, false, false>,
-    launch<false, false, true, false>,  launch<true, false, true, false>,
-    launch<false, true, true, false>,   launch<true, true, true, false>,
-    launch<false, false, false, true>,  launch<true, false, false, true>,
-    launch<false, true, false, true>,   launch<true, true, false, true>,
-    launch<false, false, true, true>,   launch<true, false, true, true>,
-    launch<false, true, true, true>,    launch<true, true, true, true>,
-    launch<false, false, false, false>, launch<true, false, false, false>,
-    launch<false, true, false, false>,  launch<true, true, false, false>,
-    launch<false, false, true, false, true>,  launch<true, false, true, false, true>,
-    launch<false, true, true, false, true>,   launch<true, true, true, false, true>,
-    launch<false, false, false, true>,  launch<true, false, false, true>,
-    launch<false, true, false, true>,   launch<true, true, false, true>,
-    launch<false, false, true, true, true>,   launch<true, false, true, true, true>,
-    launch<false, true, true, true, true>,    launch<true, true, true, true, true>,
+// index: open | unit<<1 | bvh<<2 | stats<<3 | grid<<4 | lds<<5 (grid: the layer
+// grid walk, a build of its own; lds: its grid copied into LDS; without bvh
+// the grid bits select the scan)
+#define RT_L4(b, s) launch<false, false, b, s>, launch<true, false, b, s>, launch<false, true, b, s>, \
+                    launch<true, true, b, s>
+#define RT_G4(s, l) launch<false, false, true, s, true, l>, launch<true, false, true, s, true, l>, \
+                    launch<false, true, true, s, true, l>, launch<true, true, true, s, true, l>
+const launch_fn kLaunch[64] = {
+    RT_L4(false, false), RT_L4(true, false), RT_L4(false, true), RT_L4(true, true),      // grid 0, lds 0
+    RT_L4(false, false), RT_G4(false, false), RT_L4(false, true), RT_G4(true, false),    // grid 1, lds 0
+    RT_L4(false, false), RT_L4(true, false), RT_L4(false, true), RT_L4(true, true),      // grid 0, lds 1
+    RT_L4(false, false), RT_G4(false, true), RT_L4(false, true), RT_G4(true, true),      // grid 1, lds 1
 };
+#undef RT_L4
+#undef RT_G4
 
 void free_scene(rt_context *c) {
   (void)hipFree(c->d_geom);
@@ -1691,6 +1713,8 @@ void free_scene(rt_context *c) {
   c->d_grid_cells = nullptr;
   c->d_grid_items = nullptr;
   c->grid_nx = c->grid_nz = 0;
+  c->grid_n_items = 0;
+  c->grid_lds = false;
   c->d_geom = c->d_bvh_geom = nullptr;
   c->d_nodes = nullptr;
   c->d_orig = nullptr;
@@ -1830,6 +1854,11 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
   if (e == hipSuccess && !bb.grid_cells.empty()) {
     e = upload_vec(&c->d_grid_cells, bb.grid_cells, c->stream);
     if (e == hipSuccess) e = upload_vec(&c->d_grid_items, bb.grid_items, c->stream);
+    c->grid_n_items = bb.grid_items.size() / 4;
+    // u16 cells need first < 4096; RTOW_GRID_LDS=0 keeps the grid in global memory
+    c->grid_lds = c->grid_n_items < 4096 &&
+                  rtk::grid_lds_bytes((int)c->grid_n_items, bb.grid_nx * bb.grid_nz) <= rtk::kGridLdsMax &&
+                  bvh_builder::env_double("RTOW_GRID_LDS", 1.0, 0.0, 1.0) != 0.0;
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) {
@@ -1920,6 +1949,8 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
   kp.n_extra_pairs = (int)c->n_extra_pairs;
   kp.grid_cells = c->d_grid_cells;
   kp.grid_items = (const rtk::f4 *)c->d_grid_items;
+  kp.grid_n_items = (int)c->grid_n_items;
+  kp.grid_n_cells = c->grid_nx * c->grid_nz;
   kp.grid_x0 = c->grid_x0;
   kp.grid_xi = c->grid_xi;
   kp.grid_zi = c->grid_zi;
@@ -1952,7 +1983,8 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
                 ((prm->flags & RT_FLAG_METAL_UNIT_VECTOR) ? 2 : 0) |
                 ((prm->flags & RT_FLAG_ACCEL_BVH) ? 4 : 0) |
                 ((prm->flags & RT_FLAG_COUNT_WORK) ? 8 : 0) |
-                ((c->d_grid_cells && !(prm->flags & RT_FLAG_LAYER_BVH)) ? 16 : 0);
+                ((c->d_grid_cells && !(prm->flags & RT_FLAG_LAYER_BVH)) ? 16 : 0) |
+                ((c->d_grid_cells && c->grid_lds && !(prm->flags & RT_FLAG_LAYER_BVH)) ? 32 : 0);
   // sample chunks (RT_CHUNK_SPP) and how many waves share a tile's chunks.
   // One wave per tile traces all of a pixel's samples in sequence; when a
   // rank holds few tiles (a 1/8 share of a 4K frame is ~2.3 waves per wave
@@ -2016,7 +2048,7 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
         pk.chunks_per_unit = 1;
         pk.tile_cost = d_cost;
         pk.counters = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(d_cost) + cost_bytes);
-        kLaunch[(v & 23) | 8](blocks, st, pk, c, accum_rgb, nullptr);
+        kLaunch[(v & 55) | 8](blocks, st, pk, c, accum_rgb, nullptr);
         e = hipGetLastError();
       }
       if (e == hipSuccess && c->d_order) e = hipFreeAsync(c->d_order, st);

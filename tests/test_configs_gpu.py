@@ -201,3 +201,20 @@ def test_pilot_first_render_is_asynchronous_and_correct(rtow):
             ctx.render_async(cam, p, t.data_ptr(), st.cuda_stream)  # cached order
             torch.cuda.synchronize(dev)
             assert np.array_equal(t.cpu().numpy(), want), (w, h)
+
+
+def test_lds_resident_grid_equals_global_grid(rtow, gpu_ctx, monkeypatch):
+    """The layer grid copied into LDS (render_kernel GLDS build, the default
+    when it fits 17 KB) and the same grid read from global memory
+    (RTOW_GRID_LDS=0 at upload) give the same bits, with split chunks and the
+    pilot schedule too."""
+    cam = rtow.camera_cpu(aspect=640 / 360)
+    outs = []
+    for lds in ("0", "1"):
+        monkeypatch.setenv("RTOW_GRID_LDS", lds)
+        gpu_ctx.upload(rtow.final_scene())
+        for flags, units in ((GRID, 1), (GRID | rtow.RT_FLAG_PILOT_SCHEDULE, 3)):
+            outs.append(gpu_ctx.render(cam, rtow.make_params(640, 360, 130, seed=21, flags=flags, units=units)))
+    ref, sref = outs[0]
+    for img, st in outs[1:]:
+        same(ref, sref, img, st)
