@@ -411,14 +411,28 @@ __device__ __forceinline__ int lane_now() {
   return l;
 }
 
-// running closest hit of one lane (hittable_list::hit's closest_so_far/rec)
+// running closest hit of one lane (hittable_list::hit's closest_so_far/rec),
+// kept as the 64-bit key the candidate rule orders by: (tmax bits, tie2 | near).
+// tmax >= t_min > 0 (or +inf: no hit), so its bits order like its value; tie2
+// = 2 (0x7fffffff - index) for the closed interval (ties to the larger index)
+// or 2 index for the open one (ties to the smaller); near: the winner was taken
+// at its entering root.  One 64-bit compare decides "closer, ties by index"
+// (same sphere twice: equal keys, no update).
 struct hit_state {
   float tmax;
-  int best;  // original sphere index, -1 = miss
-  int near;  // 1: the winner was taken at its entering root (an int, not a
-             // bool: a loop-carried bool becomes an SGPR lane mask merged with
-             // exec on every node of the walk)
+  uint32_t lo;  // tie2 | near; 0xffffffff with tmax = +inf: no hit
 };
+template <bool OPEN>
+__device__ __forceinline__ uint32_t tie2_of(uint32_t idx) {
+  return OPEN ? idx << 1 : (0x7fffffffu - idx) << 1;
+}
+template <bool OPEN>
+__device__ __forceinline__ int best_of(const hit_state &hs) {
+  if (hs.tmax == __builtin_huge_valf()) return -1;
+  return (int)(OPEN ? hs.lo >> 1 : 0x7fffffffu - (hs.lo >> 1));
+}
+__device__ __forceinline__ int near_of(const hit_state &hs) { return (int)(hs.lo & 1u); }
+__device__ __forceinline__ hit_state no_hit() { return hit_state{__builtin_huge_valf(), 0xffffffffu}; }
 
 // closest-hit candidate update (sphere.h:34-44 with a = |d|^2 = 1).  The root
 // a sphere offers is t0 if t0 is past t_min, else t1; it wins if it is closer
@@ -426,20 +440,22 @@ struct hit_state {
 // the FIRST for src/gpu's open one.  This makes the result independent of the
 // order spheres are visited in: brute-force scan and BVH traversal agree bit
 // for bit.
+// tie2 = tie2_of<OPEN>(index).
 template <bool OPEN>
-__device__ __forceinline__ void candidate(bool c, float h, float disc, int idx, hit_state &hs) {
+__device__ __forceinline__ void candidate(bool c, float h, float disc, uint32_t tie2, hit_state &hs) {
   if (c) {
     const float sq = sqrt_k(disc);
     const float t0 = h - sq, t1 = h + sq;
     const bool use0 = OPEN ? (t0 > 0.001f) : (t0 >= 0.001f);
     const float root = use0 ? t0 : t1;
-    const bool above = OPEN ? (root > 0.001f) : (root >= 0.001f);
-    const bool closer =
-        (root < hs.tmax) | ((root == hs.tmax) & (OPEN ? (idx < hs.best) : (idx > hs.best)));
-    if (above & closer) {
+    // root >= t_min  <=>  t1 >= t_min (t1 >= t0; with use0, t0 >= t_min)
+    const bool above = OPEN ? (t1 > 0.001f) : (t1 >= 0.001f);
+    const uint32_t lo = tie2 + (use0 ? 1u : 0u);
+    const uint64_t key = ((uint64_t)__float_as_uint(root) << 32) | lo;
+    const uint64_t cur = ((uint64_t)__float_as_uint(hs.tmax) << 32) | hs.lo;
+    if (above & (key < cur)) {
       hs.tmax = root;
-      hs.best = idx;
-      hs.near = use0 ? 1 : 0;
+      hs.lo = lo;
     }
   }
 }
@@ -489,8 +505,8 @@ __device__ __forceinline__ void scan_pairs(const RT_CONST pair_geom *__restrict_
       const int s0 = slot0 + 2 * j;
       const int i0 = orig ? orig[s0] : s0;
       const int i1 = orig ? orig[s0 + 1] : s0 + 1;
-      candidate<OPEN>(c[2 * j], h[j].x, e[j].x - q[j].ks.x, i0, hs);
-      candidate<OPEN>(c[2 * j + 1], h[j].y, e[j].y - q[j].ks.y, i1, hs);
+      candidate<OPEN>(c[2 * j], h[j].x, e[j].x - q[j].ks.x, tie2_of<OPEN>((uint32_t)i0), hs);
+      candidate<OPEN>(c[2 * j + 1], h[j].y, e[j].y - q[j].ks.y, tie2_of<OPEN>((uint32_t)i1), hs);
     }
   }
 }
@@ -635,7 +651,9 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
       if (STATS && RT_COUNT_ITEMS == 2 && __builtin_amdgcn_ballot_w64(e >= it.z) &&
           lane_now() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true)))
         ++wc.box_hits;
-      candidate<OPEN>(e >= it.z, h, e - it.z, __float_as_int(it.w), hs);
+      // it.w holds tie2_of<false>(index); the open interval's is 0xfffffffe - it
+      const uint32_t w = __float_as_uint(it.w);
+      candidate<OPEN>(e >= it.z, h, e - it.z, OPEN ? 0xfffffffeu - w : w, hs);
       if (STATS) ++wc.tests;
     }
     // v_min_f32 written out: fminf would first canonicalise all four operands
@@ -671,7 +689,7 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
   const float nk1 = -dot3(ox, oy, oz, dx, dy, dz);
   const float o2 = dot3(ox, oy, oz, ox, oy, oz);
   const float ox2 = -2.0f * ox, oy2 = -2.0f * oy, oz2 = -2.0f * oz;
-  hit_state hs{__builtin_huge_valf(), -1, 1};
+  hit_state hs = no_hit();
   const ray_pre rp{{dx, dx}, {dy, dy}, {dz, dz}, {nk1, nk1},
                    {o2, o2}, {ox2, ox2}, {oy2, oy2}, {oz2, oz2}};
   // the BVH boxes are padded for ray origins within |O| <= oref (see
@@ -839,7 +857,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   }
 
   while (true) {
-    hit_state hs{__builtin_huge_valf(), -1, 1};
+    hit_state hs = no_hit();
     if (!__ballot(alive)) break;
     if (alive) hs = closest_hit<OPEN, BVH, STATS, GRID, GLDS>(ox, oy, oz, dx, dy, dz, wc);
     ++steps;
@@ -849,8 +867,8 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
       const float o2 = dot3(ox, oy, oz, ox, oy, oz);
       const float ox2 = -2.0f * ox, oy2 = -2.0f * oy, oz2 = -2.0f * oz;
       const float tmax = hs.tmax;
-      const int best = hs.best;
-      const bool near = hs.near;
+      const int best = best_of<OPEN>(hs);
+      const bool near = near_of(hs) != 0;
       // One hash per lane and step: a hit draws its bounce, pcg4d(pix, sample,
       // depth + 1); a miss ends the path and draws the next sample's camera
       // ray, pcg4d(pix, sample + 1, 0) (the same values as drawing each where
@@ -1095,14 +1113,14 @@ __global__ __launch_bounds__(64) void kat_kernel(int kind, const double *__restr
     const float h = fmaf(sr.cz, dz, fmaf(sr.cx, dx, fmaf(sr.cy, dy, nk1)));
     const float g = fmaf(sr.cz, oz2, fmaf(sr.cx, ox2, fmaf(sr.cy, oy2, o2)));
     const float e = fmaf(h, h, -g);
-    hit_state hs{__builtin_huge_valf(), -1, 1};
-    candidate<false>(e >= sr.ks, h, e - sr.ks, 0, hs);
-    if (hs.best < 0) return;
+    hit_state hs = no_hit();
+    candidate<false>(e >= sr.ks, h, e - sr.ks, tie2_of<false>(0u), hs);
+    if (best_of<false>(hs) < 0) return;
     float b_unused;
-    const float t = refine_root(sr, hs.tmax, hs.near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2, b_unused);
+    const float t = refine_root(sr, hs.tmax, near_of(hs) != 0, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2, b_unused);
     const float px = fmaf(t, dx, ox), py = fmaf(t, dy, oy), pz = fmaf(t, dz, oz);
     float nx = (px - sr.cx) * sr.inv_r, ny = (py - sr.cy) * sr.inv_r, nz = (pz - sr.cz) * sr.inv_r;
-    const bool front = (hs.near != 0) != (sr.inv_r < 0.0f);
+    const bool front = (near_of(hs) != 0) != (sr.inv_r < 0.0f);
     if (!front) {
       nx = -nx;
       ny = -ny;
@@ -1585,9 +1603,10 @@ struct bvh_builder {
           grid_items.push_back(s->cx[i]);
           grid_items.push_back(s->cz[i]);
           grid_items.push_back((float)(x * x + y * y + z * z - r * r));
-          int32_t idx = (int32_t)i;
+          // the tie key of the closed interval: 2 (0x7fffffff - index)
+          const uint32_t tie2 = (0x7fffffffu - i) << 1;
           float f;
-          std::memcpy(&f, &idx, 4);
+          std::memcpy(&f, &tie2, 4);
           grid_items.push_back(f);
         }
       }
