@@ -159,6 +159,7 @@ struct kparams {
 
 // the dynamic LDS of the GLDS builds: grid items, then the u16 cells
 extern __shared__ f4 s_grid_dyn[];
+typedef const __attribute__((address_space(3))) f4 lds_f4;
 __host__ __device__ constexpr size_t grid_lds_bytes(int n_items, int n_cells) {
   return (size_t)n_items * 16u + ((size_t)n_cells * 2u + 15u) / 16u * 16u;
 }
@@ -642,9 +643,17 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
       ++wc.boxes;
       if (!RT_COUNT_ITEMS && lane_now() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true))) ++wc.box_hits;
     }
-    for (uint32_t k = 0; k < cnt; ++k) {
+    // items [first, first + cnt).  GLDS: the loop runs on the LDS item
+    // pointer alone, compared with an end the compiler cannot see through
+    // (else it rewrites the exit into a separate counter: one VALU more);
+    // the LDS cells hold the items' LDS address / 16 (see the block's copy)
+    lds_f4 *ip = GLDS ? (lds_f4 *)(uintptr_t)(first << 4) : nullptr;
+    lds_f4 *ie = ip + cnt;
+    if (GLDS) asm volatile("" : "+v"(ie));
+    uint32_t k = 0;
+    if (cnt) do {
       if (STATS && RT_COUNT_ITEMS == 1 && lane_now() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true))) ++wc.box_hits;
-      const f4 it = GLDS ? s_grid_dyn[first + k] : items[first + k];
+      const f4 it = GLDS ? *ip : items[first + k];
       const float h = fmaf(it.y, dz, fmaf(it.x, dx, rl.nk1.x));
       const float g = fmaf(it.y, rl.oz2.x, fmaf(it.x, rl.ox2.x, rl.o2.x));
       const float e = fmaf(h, h, -g);
@@ -655,19 +664,20 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
       const uint32_t w = __float_as_uint(it.w);
       candidate<OPEN>(e >= it.z, h, e - it.z, OPEN ? 0xfffffffeu - w : w, hs);
       if (STATS) ++wc.tests;
-    }
-    // v_min_f32 written out: fminf would first canonicalise all four operands
-    float tnext, lim;
-    asm("v_min_f32 %0, %1, %2" : "=v"(tnext) : "v"(tmx), "v"(tmz));
+      ++ip;
+      ++k;
+    } while (GLDS ? ip != ie : k < cnt);
+    // one compare picks the step axis and the next boundary (tmx == tmz
+    // steps z, as before); v_min_f32 written out: fminf would first
+    // canonicalise its operands
+    const bool sx = tmx < tmz;
+    const float tnext = sx ? tmx : tmz;
+    float lim;
     asm("v_min_f32 %0, %1, %2" : "=v"(lim) : "v"(tb), "v"(hs.tmax));
     if (tnext > lim) break;
-    if (tmx < tmz) {
-      cell += dcx;
-      tmx += tdx;
-    } else {
-      cell += dcz;
-      tmz += tdz;
-    }
+    cell += sx ? dcx : dcz;
+    if (sx) tmx += tdx;
+    else tmz += tdz;
   }
 }
 
@@ -839,7 +849,9 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
     for (int i = (int)threadIdx.x; i < p.grid_n_items; i += kBlock) s_grid_dyn[i] = gi[i];
     uint16_t *sc = reinterpret_cast<uint16_t *>(s_grid_dyn + p.grid_n_items);
     const RT_GLOBAL uint32_t *gc = as_global(p.grid_cells);
-    for (int i = (int)threadIdx.x; i < p.grid_n_cells; i += kBlock) sc[i] = (uint16_t)gc[i];
+    // cell = (first item << 4 | count) -> ((LDS address of the first item) / 16 << 4 | count)
+    const uint32_t base16 = (uint32_t)(uintptr_t)(lds_f4 *)s_grid_dyn >> 4;
+    for (int i = (int)threadIdx.x; i < p.grid_n_cells; i += kBlock) sc[i] = (uint16_t)(gc[i] + (base16 << 4));
     __syncthreads();
   }
   // (col, global row) of this lane's pixel from pix: col from the tile origin,
