@@ -313,17 +313,12 @@ void sincos_turn(float u, float &s, float &c) {
   c = ((q + 1) & 2) ? -c0 : c0;
 }
 
-// u^(1/3) without division: inverse-cube-root seed + 4 Newton steps, u * y^2
-float cbrt01(float u) {
-  uint32_t i;
-  std::memcpy(&i, &u, 4);
-  i = 0x54a2fa8cu - i / 3u;
-  float y;
-  std::memcpy(&y, &i, 4);
-  const float u3 = u * 0.333333343f;
-  for (int k = 0; k < 4; ++k) y = y * fmaf_(-u3, (y * y) * y, 1.33333337f);
-  const float c = u * (y * y);
-  return u == 0.0f ? 0.0f : c;
+// the kernel's radius of a uniform point in the unit ball (radius law of
+// random_in_unit_sphere, vec3.h:105-112: CDF r^3): the largest of three
+// uniforms -- the hash's z and w draws and the low bytes of x, y, z
+float ball_radius(const u4 &r) {
+  const uint32_t lo = ((r.x & 0xffu) << 24) | ((r.y & 0xffu) << 16) | ((r.z & 0xffu) << 8);
+  return std::fmax(std::fmax(unif(r.z), unif(r.w)), unif(lo));
 }
 
 // sqrtf(max(x, 2^-96)): the kernel's sqrt_k (rt_render.hip) -- correctly
@@ -550,7 +545,7 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
         for (int a = 0; a < 3; ++a) rf[a] = fmaf_(kk, nn[a], d[a]);
         unit_vec(unif(r.x), unif(r.y), u[0], u[1], u[2]);
         float fz = sc.param[b];
-        if (!k.metal_unit) fz *= cbrt01(unif(r.z));
+        if (!k.metal_unit) fz *= ball_radius(r);
         for (int a = 0; a < 3; ++a) sd[a] = fmaf_(fz, u[a], rf[a]);
         scattered = dot3(sd[0], sd[1], sd[2], nn[0], nn[1], nn[2]) > 0.0f;
         th[0] *= sc.ar[b];
@@ -559,8 +554,8 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
       } else {
         const float ratio = front ? sc.inv_param[b] : sc.param[b];
         const float cos_t = std::fmin(-dot3(d[0], d[1], d[2], nn[0], nn[1], nn[2]), 1.0f);
-        const float sin_t = sqrt_k(fmaf_(-cos_t, cos_t, 1.0f));
-        const bool cannot = ratio * sin_t > 1.0f;
+        // ratio sin > 1 (material.h:64), squared (the kernel's form)
+        const bool cannot = (ratio * ratio) * fmaf_(-cos_t, cos_t, 1.0f) > 1.0f;
         const float r0 = sc.r0[b];  // ((1-ior)/(1+ior))^2, same for ior and 1/ior
         const float x = 1.0f - cos_t;
         const float x2 = x * x;

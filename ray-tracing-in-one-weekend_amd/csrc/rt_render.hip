@@ -276,17 +276,13 @@ __device__ __forceinline__ void sincos_turn(float u, float &s, float &c) {
   c = ((q + 1) & 2) ? -c0 : c0;
 }
 
-// cube root of u in [0,1) without a division: inverse-cube-root seed from the
-// exponent bits, 4 Newton steps y <- y (4/3 - (u/3) y^3), then u * y^2.  Same
-// ops on the host restatement.  (Replaces the rejection loop's radius law of
-// random_in_unit_sphere, vec3.h:105-112: |p| = u^(1/3) for a uniform ball.)
-__device__ __forceinline__ float cbrt01(float u) {
-  float y = __uint_as_float(0x54a2fa8cu - __float_as_uint(u) / 3u);
-  const float u3 = u * 0.333333343f;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) y = y * fmaf(-u3, (y * y) * y, 1.33333337f);
-  const float c = u * (y * y);
-  return u == 0.0f ? 0.0f : c;
+// Radius of a uniform point in the unit ball (the radius law of
+// random_in_unit_sphere's rejection loop, vec3.h:105-112: CDF r^3): the largest of three independent uniforms, from the step hash's
+// z and w draws and its unused low bytes of x, y, z (unif() takes the top 24
+// bits).  One v_max3 instead of a cube root.
+__device__ __forceinline__ float ball_radius(const uint4 r) {
+  const uint32_t lo = ((r.x & 0xffu) << 24) | ((r.y & 0xffu) << 16) | ((r.z & 0xffu) << 8);
+  return fmaxf(fmaxf(unif(r.z), unif(r.w)), unif(lo));
 }
 
 // (rho cos 2 pi u, rho sin 2 pi u), rho = sqrt_k(a): the polar draw of both
@@ -949,7 +945,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         } else if (sr.kind == RT_METAL) {
           // material.h:40-46
           float fz = sr.param;
-          if (!METAL_UNIT) fz *= cbrt01(unif(r.z));  // random_in_unit_sphere
+          if (!METAL_UNIT) fz *= ball_radius(r);  // random_in_unit_sphere
           sx = fmaf(fz, ux, rx);
           sy = fmaf(fz, uy, ry);
           sz = fmaf(fz, uz, rz);
@@ -958,8 +954,8 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           // dielectric, material.h:57-87 (r0 is the same for ior and 1/ior)
           const float ratio = front ? sr.inv_param : sr.param;
           const float cos_t = fminf(-dn, 1.0f);
-          const float sin_t = sqrt_k(fmaf(-cos_t, cos_t, 1.0f));
-          const bool cannot = ratio * sin_t > 1.0f;
+          // ratio sin > 1 (material.h:64), squared: no square root
+          const bool cannot = (ratio * ratio) * fmaf(-cos_t, cos_t, 1.0f) > 1.0f;
           if (cannot || schlick(cos_t, sr.r0) > unif(r.x)) {
             sx = rx;
             sy = ry;
