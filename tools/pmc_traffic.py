@@ -16,9 +16,21 @@ kernel name and averaged per dispatch.
 import argparse
 import csv
 import glob
+import hashlib
 import json
 import os
 from collections import defaultdict
+
+
+KERNEL_SRC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                          "ray-tracing-in-one-weekend_amd", "csrc", "rt_render.hip")
+
+
+def kernel_source_sha16(path=KERNEL_SRC):
+    """Fingerprint of the kernel source the counters were collected on: bench.py
+    compares it with the tree it runs from and flags a stale summary."""
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
 def main():
@@ -39,15 +51,22 @@ def main():
     grid = max((int(r["Grid_Size"]) for r in rows), default=0)
     vals = defaultdict(list)
     dur = {}
-    for r in rows:
+    for r in sorted(rows, key=lambda r: int(r["Dispatch_Id"])):
         if int(r["Grid_Size"]) != grid:
             continue
         vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
         if r.get("Start_Timestamp") and r.get("End_Timestamp"):
             dur[(r["Counter_Name"], r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
-    avg = {k: sum(v) / len(v) for k, v in vals.items()}
+    # steady state: the first full-size dispatch of a pass is the bench's warmup
+    # frame (first touch of the frame tile: its WRITE_SIZE has read up to 2.5x
+    # the timed frames'), so it is dropped when later ones exist; median of the rest
+    def steady(v):
+        v = sorted(v[1:] if len(v) > 1 else v)
+        return v[len(v) // 2] if len(v) % 2 else 0.5 * (v[len(v) // 2 - 1] + v[len(v) // 2])
+    avg = {k: steady(v) for k, v in vals.items()}
     out = {"kernel": a.kernel, "workload": a.workload, "grid_size": grid, "counters_avg_per_dispatch": avg,
-           "dispatches": {k: len(v) for k, v in vals.items()}}
+           "dispatches": {k: len(v) for k, v in vals.items()},
+           "per_dispatch": dict(vals), "statistic": "median over full-size dispatches after the first (warmup)", "kernel_source_sha16": kernel_source_sha16()}
     g = [dur[k] for k in dur if k[0] == "GRBM_GUI_ACTIVE"]
     if "GRBM_GUI_ACTIVE" in avg and g:
         # GRBM_GUI_ACTIVE is summed over the 8 XCDs

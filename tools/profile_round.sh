@@ -14,13 +14,13 @@ mkdir -p $out
 cd /tmp && export TMPDIR=/tmp
 B="$GRAFT_REPO_ROOT/bench.py --no-cpu-baseline $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/kt -o kt -- python3 $B > $out/kt.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/fetch -o fetch -- python3 $B --steps 1 > $out/fetch.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/write -o write -- python3 $B --steps 1 > $out/write.log 2>&1
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES --output-format csv -d $out/sq -o sq -- python3 $B --steps 1 > $out/sq.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/fetch -o fetch -- python3 $B --steps 3 > $out/fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $out/write -o write -- python3 $B --steps 3 > $out/write.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVES --output-format csv -d $out/sq -o sq -- python3 $B --steps 3 > $out/sq.log 2>&1
 cd $GRAFT_REPO_ROOT
-# the timed kernel: the layer grid build (bench default); KERNEL overrides
-# (e.g. "render_kernel<false, false, true, false, false>" for --accel layer_bvh)
-K=${KERNEL:-"render_kernel<false, false, true, false, true>"}
+# the timed kernel: the LDS-resident layer grid build (bench default); KERNEL overrides
+# (e.g. "render_kernel<false, false, true, false, false, false>" for --accel layer_bvh)
+K=${KERNEL:-"render_kernel<false, false, true, false, true, true>"}
 python3 tools/pmc_traffic.py $out/fetch $out/write $out/sq --kernel "$K" \
   --workload "$(grep '"metric"' $out/kt.log | tail -1 | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["config"]["workload"])')" \
   --out $out/pmc_traffic.json
