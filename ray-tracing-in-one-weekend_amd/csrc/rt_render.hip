@@ -152,8 +152,8 @@ struct kparams {
   float grid_x1, grid_z1, grid_g, grid_invg;
   int grid_nx, grid_nz;    // cells including the ring
   // LDS-resident grid (render_kernel<..., GLDS>): the block copies the items
-  // (16 B) and then the cells (as u16: first << 4 | count, first < 4096) into
-  // dynamic LDS at launch
+  // (16 B) and then n_cells + 1 u16 item-start addresses (cell i's items are
+  // [start_i, start_{i+1})) into dynamic LDS at launch
   int grid_n_items, grid_n_cells;
 };
 
@@ -161,7 +161,7 @@ struct kparams {
 extern __shared__ f4 s_grid_dyn[];
 typedef const __attribute__((address_space(3))) f4 lds_f4;
 __host__ __device__ constexpr size_t grid_lds_bytes(int n_items, int n_cells) {
-  return (size_t)n_items * 16u + ((size_t)n_cells * 2u + 15u) / 16u * 16u;
+  return (size_t)n_items * 16u + ((size_t)(n_cells + 1) * 2u + 15u) / 16u * 16u;
 }
 // LDS budget of the grid copy: 3 KB of static LDS + this stays within 20 KB
 // per 256-thread block, so 8 blocks (8 waves per SIMD) still fit in 160 KB
@@ -241,8 +241,12 @@ __device__ __forceinline__ float unif(uint32_t x) { return (float)(x >> 8) * 0x1
 // call site can tell the clamp from sqrtf (arguments are 0 or >> 2^-96, and a
 // root 2^-48 instead of 0 rounds away against any t >= 0.001); the host
 // restatement applies the same clamp anyway.
-__device__ __forceinline__ float sqrt_k(float x) {
-  x = fmaxf(x, 0x1p-96f);
+// sqrt_nc: the same without the clamp, for the candidate roots h -+ sq only
+// (x >= 0 there).  An argument below 2^-96 gives some sq < 2^-48 instead of
+// 2^-48: if |h| >= 2^-20 both round h -+ sq to h, and otherwise t1 < t_min
+// rejects the sphere either way -- the same outcome as sqrt_k, one VALU less
+// per candidate sequence (the host restatement keeps the clamp).
+__device__ __forceinline__ float sqrt_nc(float x) {
   const float y = __builtin_amdgcn_sqrtf(x);
   const float ydn = __uint_as_float(__float_as_uint(y) - 1u);
   const float yup = __uint_as_float(__float_as_uint(y) + 1u);
@@ -250,6 +254,7 @@ __device__ __forceinline__ float sqrt_k(float x) {
   r = (fmaf(-yup, y, x) > 0.0f) ? yup : r;
   return r;
 }
+__device__ __forceinline__ float sqrt_k(float x) { return sqrt_nc(fmaxf(x, 0x1p-96f)); }
 
 // sin/cos of 2*pi*u, u in [0,1): quadrant from 4u (exact), Taylor on [0,pi/2).
 __device__ __forceinline__ void sincos_turn(float u, float &s, float &c) {
@@ -441,7 +446,7 @@ __device__ __forceinline__ hit_state no_hit() { return hit_state{__builtin_huge_
 template <bool OPEN>
 __device__ __forceinline__ void candidate(bool c, float h, float disc, uint32_t tie2, hit_state &hs) {
   if (c) {
-    const float sq = sqrt_k(disc);
+    const float sq = sqrt_nc(disc);
     const float t0 = h - sq, t1 = h + sq;
     const bool use0 = OPEN ? (t0 > 0.001f) : (t0 >= 0.001f);
     const float root = use0 ? t0 : t1;
@@ -614,8 +619,9 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
   const float dx = rl.dx.x, dz = rl.dz.x;
   const float px = fmaf(ta, dx, ox), pz = fmaf(ta, dz, oz);
   const int nx = p.grid_nx, nz = p.grid_nz;
-  const int cx = min(max((int)floorf((px - p.grid_x0) * p.grid_invg), 1), nx - 2);
-  const int cz = min(max((int)floorf((pz - p.grid_z0) * p.grid_invg), 1), nz - 2);
+  int cx = (int)floorf((px - p.grid_x0) * p.grid_invg), cz = (int)floorf((pz - p.grid_z0) * p.grid_invg);
+  asm("v_med3_i32 %0, %0, 1, %1" : "+v"(cx) : "s"(nx - 2));
+  asm("v_med3_i32 %0, %0, 1, %1" : "+v"(cz) : "s"(nz - 2));
   // step directions from the sign of 1/d (= the sign bit of d, also for -0)
   const bool nxs = ix < 0.0f, nzs = iz < 0.0f;
   float tmx = fmaf(fmaf((float)(cx + (nxs ? 0 : 1)), p.grid_g, p.grid_x0), ix, oix);
@@ -625,29 +631,35 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
   // and off the texture pipeline; 166 -> 157 ms)
   const RT_GLOBAL uint32_t *__restrict__ cells = as_global(p.grid_cells);
   const RT_GLOBAL f4 *__restrict__ items = as_global(p.grid_items);
-  const uint16_t *__restrict__ lcells = reinterpret_cast<const uint16_t *>(s_grid_dyn + p.grid_n_items);
+  // GLDS: the walk's cell is the LDS byte address of its start entry, so a
+  // DDA step adds +-2 or +-2 nx bytes
+  const uint32_t lcells = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint16_t *)
+                              reinterpret_cast<const uint16_t *>(s_grid_dyn + p.grid_n_items);
   // The walk stops on time alone: it leaves the inner box only at t ~ tb and
   // the next boundary is a whole cell further, so it never steps past the ring.
-  int cell = cz * nx + cx;
-  const int dcx = nxs ? -1 : 1, dcz = nzs ? -nx : nx;
+  int cell = GLDS ? (int)lcells + 2 * (cz * nx + cx) : cz * nx + cx;
+  const int dcx = (nxs ? -1 : 1) * (GLDS ? 2 : 1), dcz = (nzs ? -nx : nx) * (GLDS ? 2 : 1);
+  typedef const __attribute__((address_space(3))) uint16_t lds_u16;
   while (true) {
-    const uint32_t ce = GLDS ? (uint32_t)lcells[(uint32_t)cell] : cells[(uint32_t)cell];
-    const uint32_t first = ce >> 4, cnt = ce & 15u;
+    const uint32_t ce = GLDS ? 0u : cells[(uint32_t)cell];
+    const uint32_t first = ce >> 4;
+    const uint32_t cnt = GLDS ? 0u : ce & 15u;
     // STATS: boxes = lane-level cell visits; box_hits / roots = wave-level DDA
     // / item iterations (counted once per wave, by its first active lane)
     if (STATS) {
       ++wc.boxes;
       if (!RT_COUNT_ITEMS && lane_now() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true))) ++wc.box_hits;
     }
-    // items [first, first + cnt).  GLDS: the loop runs on the LDS item
-    // pointer alone, compared with an end the compiler cannot see through
-    // (else it rewrites the exit into a separate counter: one VALU more);
-    // the LDS cells hold the items' LDS address / 16 (see the block's copy)
-    lds_f4 *ip = GLDS ? (lds_f4 *)(uintptr_t)(first << 4) : nullptr;
-    lds_f4 *ie = ip + cnt;
+    // items [first, first + cnt).  GLDS: cell i's items are [start_i,
+    // start_{i+1}): two ds_read_u16 of adjacent entries give both LDS item
+    // addresses, with no decoding (see the block's copy); the loop runs on
+    // the item pointer alone, compared with an end the compiler cannot see
+    // through (else it rewrites the exit into a separate counter)
+    lds_f4 *ip = GLDS ? (lds_f4 *)(uintptr_t)((lds_u16 *)(uintptr_t)cell)[0] : nullptr;
+    lds_f4 *ie = GLDS ? (lds_f4 *)(uintptr_t)((lds_u16 *)(uintptr_t)cell)[1] : nullptr;
     if (GLDS) asm volatile("" : "+v"(ie));
     uint32_t k = 0;
-    if (cnt) do {
+    if (GLDS ? ip != ie : cnt != 0) do {
       if (STATS && RT_COUNT_ITEMS == 1 && lane_now() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true))) ++wc.box_hits;
       const f4 it = GLDS ? *ip : items[first + k];
       const float h = fmaf(it.y, dz, fmaf(it.x, dx, rl.nk1.x));
@@ -709,14 +721,14 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
   } else {
     // wave-uniform stackless BVH walk: a node is entered if ANY lane's ray
     // meets its (conservatively padded) box before that lane's tmax
-    // |d| components are clamped away from 0 before the reciprocal: an
-    // exactly axis-parallel ray (it happens ~20 times per 4K frame) would
-    // otherwise give slab bounds (-inf, inf - inf = NaN), and IEEE min/max
-    // then return -inf, culling a box the ray is inside.  With the clamp
-    // every slab value is finite; the ray bends by < 1e-14 over any length.
-    const float ix = __builtin_amdgcn_rcpf(fabsf(dx) < 1e-18f ? copysignf(1e-18f, dx) : dx);
-    const float iy = __builtin_amdgcn_rcpf(fabsf(dy) < 1e-18f ? copysignf(1e-18f, dy) : dy);
-    const float iz = __builtin_amdgcn_rcpf(fabsf(dz) < 1e-18f ? copysignf(1e-18f, dz) : dz);
+    // the reciprocals are clamped to +-1e18 (one v_med3): an exactly
+    // axis-parallel ray (it happens ~20 times per 4K frame) would otherwise
+    // give slab bounds (-inf, inf - inf = NaN), and IEEE min/max then return
+    // -inf, culling a box the ray is inside.  With the clamp every slab value
+    // is finite; the ray bends by < 1e-14 over any length.
+    const float ix = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(dx), -1e18f, 1e18f);
+    const float iy = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(dy), -1e18f, 1e18f);
+    const float iz = __builtin_amdgcn_fmed3f(__builtin_amdgcn_rcpf(dz), -1e18f, 1e18f);
     const float oix = -ox * ix, oiy = -oy * iy, oiz = -oz * iz;
     // the wave walks the DFS order of its majority direction octant, so
     // coherent rays visit near children first and tmax culls the rest (BVH
@@ -845,9 +857,12 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
     for (int i = (int)threadIdx.x; i < p.grid_n_items; i += kBlock) s_grid_dyn[i] = gi[i];
     uint16_t *sc = reinterpret_cast<uint16_t *>(s_grid_dyn + p.grid_n_items);
     const RT_GLOBAL uint32_t *gc = as_global(p.grid_cells);
-    // cell = (first item << 4 | count) -> ((LDS address of the first item) / 16 << 4 | count)
-    const uint32_t base16 = (uint32_t)(uintptr_t)(lds_f4 *)s_grid_dyn >> 4;
-    for (int i = (int)threadIdx.x; i < p.grid_n_cells; i += kBlock) sc[i] = (uint16_t)(gc[i] + (base16 << 4));
+    // cell i's items are [start_i, start_{i+1}) (the builder numbers every
+    // cell's first item by the running count, ring cells included): the LDS
+    // holds each start's LDS byte address, plus the end of the last cell
+    const uint32_t base = (uint32_t)(uintptr_t)(lds_f4 *)s_grid_dyn;
+    for (int i = (int)threadIdx.x; i <= p.grid_n_cells; i += kBlock)
+      sc[i] = (uint16_t)(base + ((i < p.grid_n_cells ? gc[i] >> 4 : (uint32_t)p.grid_n_items) << 4));
     __syncthreads();
   }
   // (col, global row) of this lane's pixel from pix: col from the tile origin,
@@ -1601,11 +1616,16 @@ struct bvh_builder {
       // stored with a ring of empty cells around the listed nx x nz (the
       // kernel's DDA may step one cell past the listed region before it stops)
       const int rx = nx + 2, rz = nz + 2;
+      // in stored (ring) order, every cell's first item is the running item
+      // count, ring cells included: cell rc's items are [first_rc, first_rc+1)
       grid_cells.assign((size_t)rx * rz, 0);
       grid_items.clear();
-      for (size_t c = 0; c < lists.size(); ++c) {
-        const size_t rc = (c / nx + 1) * (size_t)rx + (c % nx + 1);
-        grid_cells[rc] = (uint32_t)(grid_items.size() / 4) << 4 | (uint32_t)lists[c].size();
+      for (size_t rc = 0; rc < grid_cells.size(); ++rc) {
+        const int a = (int)(rc % rx) - 1, b = (int)(rc / rx) - 1;
+        const bool listed = a >= 0 && a < nx && b >= 0 && b < nz;
+        const size_t c = listed ? (size_t)b * nx + a : 0;
+        grid_cells[rc] = (uint32_t)(grid_items.size() / 4) << 4 | (listed ? (uint32_t)lists[c].size() : 0u);
+        if (!listed) continue;
         for (uint32_t i : lists[c]) {
           const double x = s->cx[i], y = s->cy[i], z = s->cz[i], r = s->radius[i];
           grid_items.push_back(s->cx[i]);
