@@ -27,7 +27,6 @@ Extra objects on the JSON line:
                to the oracle's fp64 restatement (kind "port")
 """
 import argparse
-import hashlib
 import json
 import os
 import subprocess
@@ -130,11 +129,6 @@ def cpu_baseline(spp, procs):
     dt = time.perf_counter() - t
     return {"value": round(segs / dt / 1e6, 4), "unit": "Mray/s", "cores": 1, "kind": "port",
             "seconds": round(dt, 3), "sample": sample + ", single thread (oracle fp64 restatement)"}
-
-
-def kernel_source_sha16():
-    with open(os.path.join(PKG, "csrc", "rt_render.hip"), "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
 def load_pmc(workload, accel="scan"):
@@ -288,8 +282,8 @@ def main():
         achieved = flops / k_avg_s / 1e12
         value = segments / elapsed / 1e6
         pmc = load_pmc(workload, a.accel)
-        # the counters are only valid for the kernel source they were collected on
-        pmc_fresh = bool(pmc) and pmc.get("kernel_source_sha16") == kernel_source_sha16()
+        # the counters are only valid for the device code they were collected on
+        pmc_fresh = bool(pmc) and pmc.get("device_code_sha16") == rtow.device_code_sha16()
         valu_insts = pmc.get("valu_insts_per_launch")
         cnt = pmc.get("counters_avg_per_dispatch", {})
         traffic = pmc.get("hbm_bytes_per_launch")
@@ -366,7 +360,7 @@ def main():
                                   "frac": round(traffic / k_avg_s / 1e9 / PEAK_HBM_GBPS, 5)}
                                  if traffic else None),
                          "pmc_source": os.path.relpath(pmc["path"], ROOT) if pmc.get("path") else None,
-                         "pmc_matches_kernel_source": pmc_fresh,
+                         "pmc_matches_device_code": pmc_fresh,
                          "culling_speedup": round(work.bf_tests / max(1, work.sphere_tests), 1),
                          "culling_speedup_basis": "brute-force ray-sphere tests (segments x spheres, "
                                                   "SURVEY 8d) / tests the walk executes; not a roofline "

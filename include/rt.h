@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 typedef enum {
   RT_OK = 0,
@@ -135,16 +135,18 @@ typedef struct {
   int32_t band_offset;
   int32_t local_rows;
   uint32_t flags;
-  /* scheduling, not semantics: split every pixel's sample chunks (see
+  /* scheduling, not semantics: split every tile's samples (whole chunks of
    * RT_CHUNK_SPP) over this many waves; 0 = choose from the tile count (1 for
    * a 4K frame on one GPU, more when a rank's share of the frame is small) */
   uint32_t units;
 } rt_params;
 
-/* Summation order of a pixel (part of the result, like the RNG): samples are
- * accumulated in order within chunks of RT_CHUNK_SPP samples, and the chunk
- * sums are added in chunk order.  Chunks can then be traced by different
- * waves (rt_params.units) without changing a single bit of the image. */
+/* Pixel sums (part of the result, like the RNG): a sample's radiance v (at
+ * most 1: albedos must lie in [0, 1]) adds trunc(v * 2^F) to its pixel's
+ * uint32 sum, F = 31 - floor(log2(spp)); the frame holds sum * 2^-F.  Integer
+ * sums do not depend on the order, so samples can be traced by any lanes,
+ * waves (rt_params.units, split in whole chunks of RT_CHUNK_SPP samples) or
+ * GPUs without changing a single bit of the image. */
 #define RT_CHUNK_SPP 64
 
 typedef struct {
@@ -203,7 +205,9 @@ void rt_context_destroy(rt_context *ctx);
 /* Copies the scene to the device (scan records, BVH, shading records) and
  * builds the BVH.  Replaces new_world<<<1,1>>> (src/gpu/main.cu:18-75).
  * Synchronises the device first: renders still running on any stream keep
- * the previous scene.  Centres must be finite, radii finite and non-zero. */
+ * the previous scene.  Centres must be finite, radii finite and non-zero,
+ * and the albedos of lambertian and metal spheres in [0, 1] (RT_ERR_INVALID
+ * otherwise: the fixed-point pixel sums need a sample's radiance <= 1). */
 int rt_scene_upload(rt_context *ctx, const rt_scene_view *scene);
 
 /* Enqueue the render kernel on `stream` (a hipStream_t, NULL = the context's

@@ -127,8 +127,10 @@ struct kparams {
   uint32_t wshift, winv;
   // sample chunks (RT_CHUNK_SPP) and their split over waves: block b traces
   // chunks [u*cpu, (u+1)*cpu) of its tiles, u = b % units, cpu = chunks_per_unit
-  int n_chunks, units, chunks_per_unit, pad_;
-  uint64_t chunk_stride;  // floats per chunk plane (local_rows * width * 3)
+  int units, chunks_per_unit;
+  // fixed-point pixel sums: a sample adds trunc(v 2^F)
+  // to its pixel's uint32 sum; the frame holds sum 2^-F
+  float qscale, qinv;  // 2^F, 2^-F with F = 31 - floor(log2(spp))
   // device buffers (rt_context; out = the caller's frame tile)
   const struct pair_geom *scan_geom;  // brute-force order
   const struct pair_geom *geom;       // BVH leaf order
@@ -136,7 +138,6 @@ struct kparams {
   const int *orig;                    // BVH slot -> original index
   const struct shade_rec *shade;
   float *out;
-  float *chunks;
   unsigned long long *counters;
   // block schedule (nullptr = launch order): block_order[blockIdx] is the
   // block of work to run, most expensive first (rt_context tile-cost pilot)
@@ -818,40 +819,38 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
 template <bool OPEN, bool METAL_UNIT, bool BVH, bool STATS, bool GRID, bool GLDS>
 __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   // Per-lane values that the bounce loop rarely needs are not kept live (VGPR
-  // pressure at 8 waves): the wave keeps its tile origin (col0, lrow0, SGPRs)
-  // and the lane its global pixel index; column, row and the s_tot slot are
-  // recomputed from lane_now() where they are used.
+  // pressure at 8 waves): the wave keeps its tile origin (col0, lrow0, SGPRs),
+  // the lane its current pixel slot, sample and global pixel index; column and
+  // row are recomputed where they are used.
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x) >> 6;
   const unsigned bid = p.block_order ? as_const(p.block_order)[blockIdx.x] : blockIdx.x;
   const int unit = (int)(bid % (unsigned)p.units);
   const int tile = (int)(bid / (unsigned)p.units) * kWavesPerBlock + wave;
   const int col0 = (tile % p.tiles_x) * kTile, lrow0 = (tile / p.tiles_x) * kTile;
-  uint32_t pix;
-  bool valid;
+  // this wave's samples: chunks [unit*cpu, (unit+1)*cpu) of RT_CHUNK_SPP each
+  const uint32_t s_begin = (uint32_t)(unit * p.chunks_per_unit) * RT_CHUNK_SPP;
+  const uint32_t s_end = min((uint32_t)((unit + 1) * p.chunks_per_unit) * RT_CHUNK_SPP, (uint32_t)p.spp);
+  // The wave's work pool: item k of [0, kend) is sample
+  // s_begin + k / 64 of the tile's pixel slot k % 64 (x = slot % 8, y = slot /
+  // 8).  A lane whose path ends takes the next item, so no lane idles while
+  // the tile has samples left; a pixel's sum is an exact integer, whichever
+  // lanes traced its samples in whatever order.
+  const uint32_t kend = (s_end > s_begin ? s_end - s_begin : 0u) << 6;
+  __shared__ uint32_t s_sum[3][kBlock];                 // the tiles' fixed-point pixel sums
+  __shared__ uint32_t s_rowpix[kWavesPerBlock][kTile];  // global pixel index of (x = 0, y)
+  bool own_valid;
   {
     const int lane = lane_now();
     const int col = col0 + (lane & (kTile - 1));
     const int lrow = lrow0 + (lane >> 3);
     const int band = lrow / p.row_block;
     const int grow = (band * p.band_stride + p.band_offset) * p.row_block + (lrow - band * p.row_block);
-    valid = col < p.width && lrow < p.local_rows && grow < p.height;
-    pix = (uint32_t)grow * (uint32_t)p.width + (uint32_t)col;
+    own_valid = col < p.width && lrow < p.local_rows && grow < p.height;
+    if ((lane & (kTile - 1)) == 0) s_rowpix[wave][lane >> 3] = (uint32_t)grow * (uint32_t)p.width + (uint32_t)col0;
   }
-  float accr = 0.f, accg = 0.f, accb = 0.f;
-  float ox = 0.f, oy = 0.f, oz = 0.f, dx = 0.f, dy = 1.f, dz = 0.f;
-  float thr = 1.f, thg = 1.f, thb = 1.f;
-  int depth = 0;
-  uint32_t sample = 0;
-  uint32_t segs = 0, steps = 0;
-  work_ctr wc;  // executed work, STATS builds only
-  // this wave's samples: chunks [unit*cpu, (unit+1)*cpu) of RT_CHUNK_SPP each
-  const uint32_t s_begin = (uint32_t)(unit * p.chunks_per_unit) * RT_CHUNK_SPP;
-  const uint32_t s_end = min((uint32_t)((unit + 1) * p.chunks_per_unit) * RT_CHUNK_SPP, (uint32_t)p.spp);
-  // two-level sum: acc* hold the current chunk's sum; unit 0 folds finished
-  // chunks into s_tot (LDS, no registers), later units store theirs for
-  // fold_chunks
-  __shared__ float s_tot[3][kBlock];
-  s_tot[0][threadIdx.x] = s_tot[1][threadIdx.x] = s_tot[2][threadIdx.x] = 0.0f;
+  s_sum[0][threadIdx.x] = s_sum[1][threadIdx.x] = s_sum[2][threadIdx.x] = 0u;
+  // slots whose pixel is in the frame (all 64 but in the last tile column / row)
+  const uint64_t vmask = __builtin_amdgcn_ballot_w64(own_valid);
   if (GLDS) {  // the block's copy of the layer grid (kparams grid_n_items)
     const RT_GLOBAL f4 *gi = as_global(p.grid_items);
     for (int i = (int)threadIdx.x; i < p.grid_n_items; i += kBlock) s_grid_dyn[i] = gi[i];
@@ -865,55 +864,89 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
       sc[i] = (uint16_t)(base + ((i < p.grid_n_cells ? gc[i] >> 4 : (uint32_t)p.grid_n_items) << 4));
     __syncthreads();
   }
-  // (col, global row) of this lane's pixel from pix: col from the tile origin,
-  // row by exact division (pix - col) / W
+  float ox = 0.f, oy = 0.f, oz = 0.f, dx = 0.f, dy = 1.f, dz = 0.f;
+  float thr = 1.f, thg = 1.f, thb = 1.f;
+  int depth = 0;
+  uint32_t slot = 0, sample = 0, pix = 0;
+  uint32_t segs = 0, steps = 0;
+  work_ctr wc;  // executed work, STATS builds only
+  // take pool item k: slot, sample and pixel; false if the slot is outside the
+  // frame (the lane then stays alive without tracing and takes another item)
+  auto take = [&](uint32_t k) -> bool {
+    slot = k & 63u;
+    sample = s_begin + (k >> 6);
+    pix = s_rowpix[wave][slot >> 3] + (slot & (kTile - 1));
+    return vmask == ~0ull || ((vmask >> slot) & 1u) != 0;
+  };
+  // (col, global row) of the lane's pixel: col from the tile origin, row by
+  // exact division (pix - col) / W
   auto pixel_cr = [&](const kparams &k, int &col, int &grow) {
-    col = col0 + (lane_now() & (kTile - 1));
+    col = col0 + (int)(slot & (kTile - 1));
     grow = (int)(((pix - (uint32_t)col) >> k.wshift) * k.winv);
   };
-  bool alive = valid && s_end > s_begin && p.max_depth > 0;  // depth 0: black, no hit test
+  uint32_t knext = 64;  // the pool's next item (wave-uniform); lane l starts with item l
+  bool alive = kend != 0 && p.max_depth > 0;  // depth 0: black, no hit test
+  bool tracing = false;
   if (alive) {
-    int col, grow;
-    pixel_cr(p, col, grow);
-    camera_ray(p, pcg4d(pix, s_begin, 0u, p.seed32), col, grow, ox, oy, oz, dx, dy, dz);
-    sample = s_begin + 1;
+    tracing = take((uint32_t)lane_now());
+    if (tracing) {
+      int col, grow;
+      pixel_cr(p, col, grow);
+      camera_ray(p, pcg4d(pix, sample, 0u, p.seed32), col, grow, ox, oy, oz, dx, dy, dz);
+    }
   }
 
   while (true) {
-    hit_state hs = no_hit();
     if (!__ballot(alive)) break;
-    if (alive) hs = closest_hit<OPEN, BVH, STATS, GRID, GLDS>(ox, oy, oz, dx, dy, dz, wc);
+    hit_state hs = no_hit();
+    if (tracing) hs = closest_hit<OPEN, BVH, STATS, GRID, GLDS>(ox, oy, oz, dx, dy, dz, wc);
     ++steps;
+    const int best = best_of<OPEN>(hs);
+    // lanes that end their path here (a miss) or hold a slot outside the frame
+    // take their next items now: the step's one hash then draws the new camera ray
+    const bool miss = alive && (!tracing || best < 0);
+    uint32_t kn;
+    {
+      const uint64_t need = __builtin_amdgcn_ballot_w64(miss);
+      kn = knext + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+      knext += (uint32_t)__builtin_popcountll(need);
+    }
+    bool path_done = false;  // absorbed, or the bounce limit: a new item below
     if (alive) {
-      ++segs;
       const kparams q = kernargs();  // shading's parameters, re-read per step
-      const float o2 = dot3(ox, oy, oz, ox, oy, oz);
-      const float ox2 = -2.0f * ox, oy2 = -2.0f * oy, oz2 = -2.0f * oz;
-      const float tmax = hs.tmax;
-      const int best = best_of<OPEN>(hs);
-      const bool near = near_of(hs) != 0;
+      if (tracing) ++segs;
+      if (tracing && best < 0) {
+        // miss: sky gradient, src/cpu/main.cc:27-29; the sample's radiance
+        // goes into its pixel's fixed-point sum
+        const float a = 0.5f * (dy + 1.0f);
+        const float s0 = 1.0f - a;
+        const int i = wave * 64 + (int)slot;
+        atomicAdd(&s_sum[0][i], (uint32_t)(thr * fmaf(a, 0.5f, s0) * q.qscale));
+        atomicAdd(&s_sum[1][i], (uint32_t)(thg * fmaf(a, 0.7f, s0) * q.qscale));
+        atomicAdd(&s_sum[2][i], (uint32_t)(thb * (s0 + a) * q.qscale));
+      }
+      if (miss) {
+        if (kn < kend) {
+          tracing = take(kn);
+        } else {
+          alive = tracing = false;
+        }
+      }
       // One hash per lane and step: a hit draws its bounce, pcg4d(pix, sample,
-      // depth + 1); a miss ends the path and draws the next sample's camera
-      // ray, pcg4d(pix, sample + 1, 0) (the same values as drawing each where
-      // it is used; only absorbed paths need a second hash below)
-      const bool miss = best < 0;
-      const uint4 r = pcg4d(pix, miss ? sample : sample - 1u, miss ? 0u : (uint32_t)(depth + 1), q.seed32);
+      // depth + 1); a lane that took a new item draws its camera ray, pcg4d(pix,
+      // sample, 0) (only absorbed paths need a second hash below)
+      const uint4 r = pcg4d(pix, sample, miss ? 0u : (uint32_t)(depth + 1), q.seed32);
       // one polar draw per lane and step: a hit's unit vector (oracle unit_vec:
-      // z = 1 - 2 u1), a miss's lens sample for its next camera ray
+      // z = 1 - 2 u1), a new camera ray's lens sample
       const float uz = fmaf(-2.0f, unif(r.x), 1.0f);
       float ux, uy;
       polar(miss ? unif(r.z) : fmaf(-uz, uz, 1.0f), unif(miss ? r.w : r.y), ux, uy);
 
-      bool path_done = false;
-      if (miss) {
-        // miss: sky gradient, src/cpu/main.cc:27-29
-        const float a = 0.5f * (dy + 1.0f);
-        const float s0 = 1.0f - a;
-        accr = fmaf(thr, fmaf(a, 0.5f, s0), accr);
-        accg = fmaf(thg, fmaf(a, 0.7f, s0), accg);
-        accb = fmaf(thb, s0 + a, accb);
-        path_done = true;
-      } else {
+      if (!miss) {
+        const float o2 = dot3(ox, oy, oz, ox, oy, oz);
+        const float ox2 = -2.0f * ox, oy2 = -2.0f * oy, oz2 = -2.0f * oz;
+        const float tmax = hs.tmax;
+        const bool near = near_of(hs) != 0;
         const shade_rec sr = cload_g(as_global(q.shade) + best);
         float b;
         const float t = refine_root(sr, tmax, near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2, b);
@@ -995,59 +1028,62 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           dz = sz;
         }
         }
+      } else if (tracing) {
+        // a new item: its camera ray, with the lens sample drawn above
+        int col, grow;
+        pixel_cr(q, col, grow);
+        camera_dir(q, r, ux, uy, col, grow, ox, oy, oz, dx, dy, dz);
+        depth = 0;
+        thr = thg = thb = 1.0f;
       }
-      if (path_done) {
-        if (sample % RT_CHUNK_SPP == 0 || sample == s_end) {  // the path closed a chunk
-          const int l = lane_now();
-          if (unit == 0) {
-            const int slot = wave * 64 + l;
-            s_tot[0][slot] += accr;
-            s_tot[1][slot] += accg;
-            s_tot[2][slot] += accb;
-          } else {
-            const int col = col0 + (l & (kTile - 1)), lrow = lrow0 + (l >> 3);
-            RT_GLOBAL float *c = as_global(q.chunks) + (size_t)((sample - 1) / RT_CHUNK_SPP) * q.chunk_stride +
-                       3 * ((size_t)lrow * q.width + col);
-            c[0] = accr;
-            c[1] = accg;
-            c[2] = accb;
-          }
-          accr = accg = accb = 0.0f;
-        }
-        if (sample < s_end) {
+    }
+    // absorbed paths and paths at the bounce limit take their next items here
+    {
+      const uint64_t need = __builtin_amdgcn_ballot_w64(path_done);
+      kn = knext + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+      knext += (uint32_t)__builtin_popcountll(need);
+    }
+    if (path_done) {
+      if (kn < kend) {
+        tracing = take(kn);
+        if (tracing) {  // the camera draw needs its own hash
           const kparams k = kernargs();  // camera re-read
           int col, grow;
           pixel_cr(k, col, grow);
-          uint4 rc = r;
-          float ddx = ux, ddy = uy;  // a miss's lens sample, drawn above
-          if (!miss) {  // absorbed or depth limit: the camera draw needs its own hash
-            rc = pcg4d(pix, sample, 0u, k.seed32);
-            if (k.cam.has_lens) polar(unif(rc.z), unif(rc.w), ddx, ddy);
-          }
+          const uint4 rc = pcg4d(pix, sample, 0u, k.seed32);
+          float ddx = 0.0f, ddy = 0.0f;
+          if (k.cam.has_lens) polar(unif(rc.z), unif(rc.w), ddx, ddy);
           camera_dir(k, rc, ddx, ddy, col, grow, ox, oy, oz, dx, dy, dz);
-          ++sample;
           depth = 0;
           thr = thg = thb = 1.0f;
-        } else {
-          alive = false;
         }
+      } else {
+        alive = tracing = false;
       }
-      // one normalize3 per lane and step: the bounce direction or the new
-      // camera ray's (a finished lane's is unused)
-      normalize3(dx, dy, dz);
     }
+    // one normalize3 per lane and step: the bounce direction or the new
+    // camera ray's (a finished lane's is unused)
+    if (alive) normalize3(dx, dy, dz);
   }
 
   const int lane = lane_now();
-  if (unit == 0) {
+  {
     const kparams q = kernargs();
     const int col = col0 + (lane & (kTile - 1)), lrow = lrow0 + (lane >> 3);
     if (col < q.width && lrow < q.local_rows) {  // padding pixels (row >= height) write zeros
-      RT_GLOBAL float *o = as_global(q.out) + 3 * ((size_t)lrow * q.width + col);
-      const int slot = wave * 64 + lane;
-      o[0] = s_tot[0][slot];
-      o[1] = s_tot[1][slot];
-      o[2] = s_tot[2][slot];
+      const size_t o = 3 * ((size_t)lrow * q.width + col);
+      const int i = wave * 64 + lane;
+      if (q.units == 1) {
+        RT_GLOBAL float *out = as_global(q.out) + o;
+        out[0] = (float)s_sum[0][i] * q.qinv;
+        out[1] = (float)s_sum[1][i] * q.qinv;
+        out[2] = (float)s_sum[2][i] * q.qinv;
+      } else {  // the tile's units add their integer sums (finish_sums converts)
+        uint32_t *acc = reinterpret_cast<uint32_t *>(q.out) + o;
+        atomicAdd(acc + 0, s_sum[0][i]);
+        atomicAdd(acc + 1, s_sum[1][i]);
+        atomicAdd(acc + 2, s_sum[2][i]);
+      }
     }
   }
   // one atomic per wave for the counters
@@ -1080,22 +1116,12 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   }
 }
 
-// out += chunk sums of the waves with unit > 0, in chunk order (the left fold
-// of RT_CHUNK_SPP's two-level sum; unit 0 already folded chunks [0, first)).
-// Memory-bound and tiny: (n_chunks - first) planes read once.
-__global__ __launch_bounds__(256) void fold_chunks(const float *__restrict__ chunks, float *__restrict__ out,
-                                                   int first, int n_chunks, uint64_t stride, int width,
-                                                   int height, int row_block, int band_stride,
-                                                   int band_offset) {
-  for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < stride; j += (uint64_t)gridDim.x * 256u) {
-    const int lrow = (int)(j / (3u * (uint64_t)width));
-    const int band = lrow / row_block;
-    const int grow = (band * band_stride + band_offset) * row_block + (lrow - band * row_block);
-    if (grow >= height) continue;  // padding rows stay zero
-    float acc = out[j];
-    for (int k = first; k < n_chunks; ++k) acc += chunks[(uint64_t)k * stride + j];
-    out[j] = acc;
-  }
+// Several waves per tile (rt_params.units > 1): they added their integer pixel
+// sums into the frame (zeroed first), which holds uint32 sums until this pass
+// converts them in place, sum * 2^-F.  Memory-bound and tiny.
+__global__ __launch_bounds__(256) void finish_sums(float *__restrict__ out, uint64_t n, float qinv) {
+  for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < n; j += (uint64_t)gridDim.x * 256u)
+    out[j] = (float)reinterpret_cast<const uint32_t *>(out)[j] * qinv;
 }
 
 // Known-answer evaluation of the render kernel's own device arithmetic
@@ -1244,16 +1270,14 @@ struct rt_context {
   unsigned long long *d_counters = nullptr;
   float *d_frame = nullptr;
   size_t frame_floats = 0;
-  float *d_chunks = nullptr;  // chunk sums of units > 0 (RT_CHUNK_SPP), grown on demand
   // block schedule from a pilot render, cached per frame geometry
   uint32_t *d_order = nullptr;
   size_t order_n = 0;
   std::vector<uint64_t> order_key;
-  size_t chunk_floats = 0;
   uint64_t last_samples = 0;
   bool last_stats = false;
   // Renders of one context may be enqueued on different streams; they share
-  // the scratch buffers above (chunk sums, block order), so each render first
+  // the scratch buffer above (block order), so each render first
   // waits for the previous one: ev_done is recorded after every render on
   // last_stream, and a render on another stream waits on it (no host sync).
   hipEvent_t ev_done = nullptr;
@@ -1718,7 +1742,7 @@ void fill_slot(rtk::pair_geom &g, int l, const rt_scene_view *s, int i) {
 }
 
 template <bool O, bool U, bool B, bool S, bool G = false, bool L = false>
-void launch(unsigned blocks, hipStream_t st, const rtk::kparams &kp0, rt_context *c, float *out, float *chunks) {
+void launch(unsigned blocks, hipStream_t st, const rtk::kparams &kp0, rt_context *c, float *out) {
   rtk::kparams kp = kp0;
   kp.scan_geom = c->d_geom;
   kp.geom = c->d_bvh_geom;
@@ -1726,13 +1750,12 @@ void launch(unsigned blocks, hipStream_t st, const rtk::kparams &kp0, rt_context
   kp.orig = c->d_orig;
   kp.shade = c->d_shade;
   kp.out = out;
-  kp.chunks = chunks;
   if (!kp.counters) kp.counters = c->d_counters;  // (the pilot brings its own)
   const size_t lds = L ? rtk::grid_lds_bytes(kp.grid_n_items, kp.grid_n_cells) : 0u;
   rtk::render_kernel<O, U, B, S, G, L><<<blocks, rtk::kBlock, lds, st>>>(kp);
 }
 
-using launch_fn = void (*)(unsigned, hipStream_t, const rtk::kparams &, rt_context *, float *, float *);
+using launch_fn = void (*)(unsigned, hipStream_t, const rtk::kparams &, rt_context *, float *);
 // index: open | unit<<1 | bvh<<2 | stats<<3 | grid<<4 | lds<<5 (grid: the layer
 // grid walk, a build of its own; lds: its grid copied into LDS; without bvh
 // the grid bits select the scan)
@@ -1839,7 +1862,6 @@ void rt_context_destroy(rt_context *c) {
   free_scene(c);
   (void)hipFree(c->d_counters);
   (void)hipFree(c->d_frame);
-  (void)hipFree(c->d_chunks);
   (void)hipFree(c->d_order);
   (void)hipFree(c->d_thr64);
   (void)hipFree(c->d_thr32);
@@ -1858,6 +1880,12 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
     if (s->mat_kind[i] > RT_DIELECTRIC || !(s->radius[i] != 0.0f) || !std::isfinite(s->radius[i]) ||
         !std::isfinite(s->cx[i]) || !std::isfinite(s->cy[i]) || !std::isfinite(s->cz[i]))
       return RT_ERR_INVALID;
+  // albedos in [0, 1] (energy-conserving materials): a sample's radiance is
+  // then at most 1, which the fixed-point pixel sums rely on (DESIGN.md 2,
+  // step 6); dielectrics ignore theirs
+  for (uint32_t i = 0; i < s->n; ++i)
+    for (int k = 0; k < 3 && s->mat_kind[i] != RT_DIELECTRIC; ++k)
+      if (!(s->albedo_rgb[3 * i + k] >= 0.0f && s->albedo_rgb[3 * i + k] <= 1.0f)) return RT_ERR_INVALID;
   const uint32_t n = s->n;
   const uint32_t n_pad = (n + rtk::kSpherePad - 1) / rtk::kSpherePad * rtk::kSpherePad;
   std::vector<rtk::pair_geom> geom(n_pad / 2);
@@ -1959,7 +1987,7 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
                    hipEvent_t ev_start) {
   RT_HIP(hipSetDevice(c->device));
   // renders of one context are serialised, whatever streams they come on:
-  // they share the chunk and block-order scratch buffers
+  // they share the block-order scratch buffer
   if (c->have_done && c->last_stream != st) RT_HIP(hipStreamWaitEvent(st, c->ev_done, 0));
   const uint64_t samples = (uint64_t)prm->width * valid_rows(prm) * (uint64_t)prm->spp;
   if (prm->flags & RT_FLAG_KEEP_COUNTERS) {
@@ -2047,24 +2075,15 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
   units = std::max(1LL, std::min<long long>(units, n_chunks));
   const int cpu = (int)((n_chunks + units - 1) / units);
   units = (n_chunks + cpu - 1) / cpu;
-  kp.n_chunks = n_chunks;
   kp.units = (int)units;
   kp.chunks_per_unit = cpu;
-  kp.chunk_stride = (uint64_t)prm->local_rows * (uint64_t)prm->width * 3u;
-  float *chunks = nullptr;
-  if (units > 1) {
-    const size_t need = (size_t)n_chunks * kp.chunk_stride;
-    if (need > c->chunk_floats) {
-      // stream-ordered: the old buffer is released after the renders already
-      // queued on st (and, through ev_done, on any other stream) have run
-      if (c->d_chunks) RT_HIP(hipFreeAsync(c->d_chunks, st));
-      c->d_chunks = nullptr;
-      c->chunk_floats = 0;
-      RT_HIP(hipMallocAsync((void **)&c->d_chunks, need * sizeof(float), st));
-      c->chunk_floats = need;
-    }
-    chunks = c->d_chunks;
+  {
+    int f = 31;  // F = 31 - floor(log2(spp)): spp samples of at most 2^F each fit a uint32
+    for (int s = prm->spp; s > 1; s >>= 1) --f;
+    kp.qscale = std::ldexp(1.0f, f);
+    kp.qinv = std::ldexp(1.0f, -f);
   }
+  const uint64_t frame_floats = (uint64_t)prm->local_rows * (uint64_t)prm->width * 3u;
   if ((prm->flags & RT_FLAG_PILOT_SCHEDULE) && prm->spp > 0 && prm->max_depth > 0 && blocks > 1) {
     // Expensive tiles first (RT_FLAG_PILOT_SCHEDULE): a 4-spp pilot (same
     // geometry, one wave per tile, the instrumented build that reports each
@@ -2090,12 +2109,11 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
       if (e == hipSuccess) {
         rtk::kparams pk = kp;
         pk.spp = std::min(prm->spp, 4);
-        pk.n_chunks = 1;
         pk.units = 1;
         pk.chunks_per_unit = 1;
         pk.tile_cost = d_cost;
         pk.counters = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(d_cost) + cost_bytes);
-        kLaunch[(v & 55) | 8](blocks, st, pk, c, accum_rgb, nullptr);
+        kLaunch[(v & 55) | 8](blocks, st, pk, c, accum_rgb);
         e = hipGetLastError();
       }
       if (e == hipSuccess && c->d_order) e = hipFreeAsync(c->d_order, st);
@@ -2112,14 +2130,15 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
     }
     kp.block_order = c->d_order;
   }
+  // several units per tile add their integer sums into the zeroed frame
+  // (after the pilot, which renders into it too), finish_sums converts them
+  if (units > 1) RT_HIP(hipMemsetAsync(accum_rgb, 0, frame_floats * sizeof(float), st));
   if (ev_start) RT_HIP(hipEventRecord(ev_start, st));
-  kLaunch[v]((unsigned)(blocks * units), st, kp, c, accum_rgb, chunks);
+  kLaunch[v]((unsigned)(blocks * units), st, kp, c, accum_rgb);
   RT_HIP(hipGetLastError());
   if (units > 1) {
-    const uint64_t n = kp.chunk_stride;
-    const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, 256u * 64u);
-    rtk::fold_chunks<<<grid, 256, 0, st>>>(chunks, accum_rgb, cpu, n_chunks, n, prm->width, prm->height,
-                                           prm->row_block, prm->band_stride, prm->band_offset);
+    const unsigned grid = (unsigned)std::min<uint64_t>((frame_floats + 255) / 256, 256u * 64u);
+    rtk::finish_sums<<<grid, 256, 0, st>>>(accum_rgb, frame_floats, kp.qinv);
     RT_HIP(hipGetLastError());
   }
   RT_HIP(hipEventRecord(c->ev_done, st));

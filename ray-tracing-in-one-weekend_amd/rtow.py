@@ -24,6 +24,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RTOW_LIB") or os.path.join(HERE, "librtow.so")
 
 RT_LAMBERTIAN, RT_METAL, RT_DIELECTRIC = 0, 1, 2
+RT_ERR_INVALID = -1
 RT_CAMERA_CPU, RT_CAMERA_GPU = 0, 1
 RT_FLAG_OPEN_INTERVAL = 1
 RT_FLAG_METAL_UNIT_VECTOR = 2
@@ -33,10 +34,10 @@ RT_FLAG_ACCEL_BVH = 1 << 9
 RT_FLAG_COUNT_WORK = 1 << 10
 RT_FLAG_PILOT_SCHEDULE = 1 << 11  # launch expensive tiles first (4-spp pilot per frame geometry)
 RT_FLAG_LAYER_BVH = 1 << 12  # layer scenes: walk the layer BVH instead of the layer grid
-RT_CHUNK_SPP = 64  # include/rt.h: samples per chunk of the two-level pixel sum
+RT_CHUNK_SPP = 64  # include/rt.h: granularity of the units split (pixel sums are exact integers)
 RT_TONEMAP_CPU, RT_TONEMAP_GPU = 0, 1  # write_color of src/cpu (fp64) / src/gpu (fp32)
 RT_KAT_SPHERE_HIT, RT_KAT_REFLECT, RT_KAT_REFRACT, RT_KAT_REFLECTANCE = 0, 1, 2, 3
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _f = ctypes.POINTER(ctypes.c_float)
 _u32 = ctypes.POINTER(ctypes.c_uint32)
@@ -139,6 +140,26 @@ class RTError(RuntimeError):
 def check(status, where):
     if status != 0:
         raise RTError(status, where)
+
+
+def device_code_sha16(path=None):
+    """Fingerprint of the gfx950 code in a built library: sha256 of its
+    .hip_fatbin section (the device code objects only; host-side edits leave it
+    unchanged, and rebuilding the same source gives the same bytes).  PMC
+    summaries record it so that bench.py can flag counters collected on other
+    kernel code."""
+    import hashlib
+    import struct
+    with open(path or LIB_PATH, "rb") as f:
+        b = f.read()
+    shoff = struct.unpack_from("<Q", b, 0x28)[0]
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
+    names = secs[shstrndx][4]
+    for s in secs:
+        if b[names + s[0]:b.index(b"\0", names + s[0])] == b".hip_fatbin":
+            return hashlib.sha256(b[s[4]:s[4] + s[5]]).hexdigest()[:16]
+    return None
 
 
 def _ptr(a, t):

@@ -218,3 +218,33 @@ def test_lds_resident_grid_equals_global_grid(rtow, gpu_ctx, monkeypatch):
     ref, sref = outs[0]
     for img, st in outs[1:]:
         same(ref, sref, img, st)
+
+
+@pytest.mark.gpu
+def test_scene_upload_rejects_albedo_outside_unit_interval(rtow):
+    """The fixed-point pixel sums need a sample's radiance
+    <= 1: rt_scene_upload refuses a lambertian or metal albedo outside [0, 1]
+    (or NaN) with RT_ERR_INVALID and keeps the previous scene; a dielectric's
+    albedo is ignored, as the kernel ignores it."""
+    import dataclasses
+    base = rtow.final_scene()
+    with rtow.Context(0) as ctx:
+        ctx.upload(base)
+        cam = rtow.camera_cpu(aspect=16 / 9)
+        prm = rtow.make_params(32, 18, 4, seed=3, flags=rtow.RT_FLAG_ACCEL_BVH)
+        before, _ = ctx.render(cam, prm)
+        lam = int(np.nonzero(base.kind == rtow.RT_LAMBERTIAN)[0][0])
+        die = int(np.nonzero(base.kind == rtow.RT_DIELECTRIC)[0][0])
+        for bad in (1.0001, -1e-7, float("nan")):
+            alb = base.albedo.copy()
+            alb[lam, 1] = bad
+            with pytest.raises(rtow.RTError) as ei:
+                ctx.upload(dataclasses.replace(base, albedo=alb))
+            assert ei.value.status == rtow.RT_ERR_INVALID
+        after, _ = ctx.render(cam, prm)
+        assert np.array_equal(before, after)  # the previous scene stayed
+        alb = base.albedo.copy()
+        alb[die] = 7.0  # ignored for a dielectric
+        ctx.upload(dataclasses.replace(base, albedo=alb))
+        same, _ = ctx.render(cam, prm)
+        assert np.array_equal(before, same)

@@ -182,7 +182,7 @@ def test_invalid_arguments_return_status(rtow):
     assert L.rt_scene_final(11, None, None) == -1
     assert L.rt_tonemap_u8(None, 4, 10, None) == -1
     assert L.rt_strerror(-4) == b"no such HIP device"
-    assert L.rt_abi_version() == rtow.ABI_VERSION == 2
+    assert L.rt_abi_version() == rtow.ABI_VERSION == 3
     with pytest.raises(rtow.RTError):
         rtow.camera_cpu(aspect=0.0)
 

@@ -217,7 +217,8 @@ def test_headline_geometry_one_spp(rtow, gpu_ctx):
 @pytest.mark.parametrize("units", [1, 2, 3])
 def test_chunked_sum_bit_exact_vs_oracle(rtow, gpu_ctx, units, accel):
     """spp > RT_CHUNK_SPP: three sample chunks (64, 64, 22), traced by 1, 2 or
-    3 waves per tile; the two-level sum matches the oracle bit for bit."""
+    3 waves per tile from each wave's sample pool; the fixed-point pixel sums
+    match the oracle bit for bit."""
     scene = rtow.final_scene()
     cam = rtow.camera_cpu(aspect=2.0)
     p = rtow.make_params(24, 12, 150, seed=17, units=units)

@@ -16,21 +16,15 @@ kernel name and averaged per dispatch.
 import argparse
 import csv
 import glob
-import hashlib
 import json
 import os
+import sys
 from collections import defaultdict
 
 
-KERNEL_SRC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
-                          "ray-tracing-in-one-weekend_amd", "csrc", "rt_render.hip")
-
-
-def kernel_source_sha16(path=KERNEL_SRC):
-    """Fingerprint of the kernel source the counters were collected on: bench.py
-    compares it with the tree it runs from and flags a stale summary."""
-    with open(path, "rb") as f:
-        return hashlib.sha256(f.read()).hexdigest()[:16]
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                "ray-tracing-in-one-weekend_amd"))
+import rtow  # noqa: E402  (device_code_sha16 only: the library is not loaded)
 
 
 def main():
@@ -66,7 +60,7 @@ def main():
     avg = {k: steady(v) for k, v in vals.items()}
     out = {"kernel": a.kernel, "workload": a.workload, "grid_size": grid, "counters_avg_per_dispatch": avg,
            "dispatches": {k: len(v) for k, v in vals.items()},
-           "per_dispatch": dict(vals), "statistic": "median over full-size dispatches after the first (warmup)", "kernel_source_sha16": kernel_source_sha16()}
+           "per_dispatch": dict(vals), "statistic": "median over full-size dispatches after the first (warmup)", "device_code_sha16": rtow.device_code_sha16()}
     g = [dur[k] for k in dur if k[0] == "GRBM_GUI_ACTIVE"]
     if "GRBM_GUI_ACTIVE" in avg and g:
         # GRBM_GUI_ACTIVE is summed over the 8 XCDs

@@ -51,6 +51,56 @@ KERN(k_xor, int, I1, "v_xor_b32 %0, %1, %0", V)
 KERN(k_mullo, int, I1, "v_mul_lo_u32 %0, %1, %0", V)
 KERN(k_cndmask, float, F1, "v_cmp_lt_f32 vcc, %1, %0\n\tv_cndmask_b32 %0, %0, %2, vcc", V)
 KERN(k_sqrt, float, F1, "v_sqrt_f32 %0, %0", V)
+KERN(k_and, int, I1, "v_and_b32 %0, %1, %0", V)
+KERN(k_lshr, int, I1, "v_lshrrev_b32 %0, %1, %0", V)
+KERN(k_ashr, int, I1, "v_ashrrev_i32 %0, %1, %0", V)
+KERN(k_bfi, int, I1, "v_bfi_b32 %0, %1, %2, %0", V)
+KERN(k_add3, int, I1, "v_add3_u32 %0, %1, %2, %0", V)
+KERN(k_lshladd, int, I1, "v_lshl_add_u32 %0, %0, 1, %1", V)
+KERN(k_madu24, int, I1, "v_mad_u32_u24 %0, %1, %2, %0", V)
+KERN(k_subf, float, F1, "v_sub_f32 %0, %1, %0", V)
+KERN(k_fmak, float, F1, "v_fmaak_f32 %0, %1, %0, 0x3f000000", V)
+KERN(k_cvt, float, F1, "v_cvt_f32_u32 %0, %0", V)
+// v_cmp alone (writes an SGPR pair) and v_cndmask alone (reads one)
+__global__ __launch_bounds__(256) void k_cmp(float *out, int iters, float b, float c) {
+  float a[8];
+  unsigned long long m = 0;
+  _Pragma("unroll") for (int k = 0; k < 8; ++k) a[k] = threadIdx.x * 1e-3f + k;
+  for (int i = 0; i < iters; ++i) {
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) {
+      unsigned long long r;
+      asm volatile("v_cmp_lt_f32_e64 %0, %1, %2" : "=s"(r) : "v"(a[k]), "v"(b));
+      m ^= r;
+    }
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = (float)(m & 1) + a[0];
+}
+__global__ __launch_bounds__(256) void k_cnd(float *out, int iters, float b, float c) {
+  float a[8];
+  const unsigned long long m = __builtin_amdgcn_ballot_w64(threadIdx.x & 1);
+  _Pragma("unroll") for (int k = 0; k < 8; ++k) a[k] = threadIdx.x * 1e-3f + k;
+  for (int i = 0; i < iters; ++i) {
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[k]) : "v"(c), "s"(m));
+  }
+  float s = 0;
+  _Pragma("unroll") for (int k = 0; k < 8; ++k) s += a[k];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+// v_mad_u64_u32 (the compiler's choice for pcg4d's x += y * w): 64-bit accumulators
+__global__ __launch_bounds__(256) void k_mad64(float *out, int iters, float b, float c) {
+  unsigned long long a[8];
+  unsigned bb = (unsigned)(b * 1e6f);
+  _Pragma("unroll") for (int k = 0; k < 8; ++k) a[k] = threadIdx.x * 7u + k;
+  for (int i = 0; i < iters; ++i) {
+    _Pragma("unroll") for (int k = 0; k < 8; ++k) {
+      unsigned long long cy;
+      asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(a[k]), "=s"(cy) : "v"((unsigned)a[k]), "v"(bb));
+    }
+  }
+  float s = 0;
+  _Pragma("unroll") for (int k = 0; k < 8; ++k) s += (float)(unsigned)a[k];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
 KERN(k_rcp, float, F1, "v_rcp_f32 %0, %0", V)
 
 #define CHK(x)                                                             \
@@ -84,7 +134,14 @@ int main() {
             {k_pkmul, "v_pk_mul_f32", 1},         {k_pkadd, "v_pk_add_f32", 1},
             {k_addu, "v_add_u32", 1},             {k_xor, "v_xor_b32", 1},
             {k_mullo, "v_mul_lo_u32", 1},         {k_cndmask, "v_cmp_lt_f32 + v_cndmask", 2},
-            {k_sqrt, "v_sqrt_f32", 1},            {k_rcp, "v_rcp_f32", 1}};
+            {k_sqrt, "v_sqrt_f32", 1},            {k_rcp, "v_rcp_f32", 1},
+            {k_and, "v_and_b32", 1},              {k_lshr, "v_lshrrev_b32", 1},
+            {k_ashr, "v_ashrrev_i32", 1},         {k_bfi, "v_bfi_b32", 1},
+            {k_add3, "v_add3_u32", 1},            {k_lshladd, "v_lshl_add_u32", 1},
+            {k_madu24, "v_mad_u32_u24", 1},       {k_subf, "v_sub_f32 (vgpr)", 1},
+            {k_fmak, "v_fmaak_f32 (literal)", 1}, {k_cvt, "v_cvt_f32_u32", 1},
+            {k_cmp, "v_cmp_lt_f32 (vcc only)", 1}, {k_cnd, "v_cndmask_b32 (vcc)", 1},
+            {k_mad64, "v_mad_u64_u32", 1}};
   const int nk = sizeof(ks) / sizeof(ks[0]);
   for (int rep = 0; rep < 2; ++rep) {
     for (int v = 0; v < nk; ++v) {
