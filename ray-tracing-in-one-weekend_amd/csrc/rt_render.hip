@@ -911,7 +911,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
       kn = knext + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
       knext += (uint32_t)__builtin_popcountll(need);
     }
-    bool path_done = false;  // absorbed, or the bounce limit: a new item below
+    bool path_done = false;  // absorbed, or the bounce limit: the lane parks for a step
     if (alive) {
       const kparams q = kernargs();  // shading's parameters, re-read per step
       if (tracing) ++segs;
@@ -1037,30 +1037,10 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         thr = thg = thb = 1.0f;
       }
     }
-    // absorbed paths and paths at the bounce limit take their next items here
-    {
-      const uint64_t need = __builtin_amdgcn_ballot_w64(path_done);
-      kn = knext + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-      knext += (uint32_t)__builtin_popcountll(need);
-    }
-    if (path_done) {
-      if (kn < kend) {
-        tracing = take(kn);
-        if (tracing) {  // the camera draw needs its own hash
-          const kparams k = kernargs();  // camera re-read
-          int col, grow;
-          pixel_cr(k, col, grow);
-          const uint4 rc = pcg4d(pix, sample, 0u, k.seed32);
-          float ddx = 0.0f, ddy = 0.0f;
-          if (k.cam.has_lens) polar(unif(rc.z), unif(rc.w), ddx, ddy);
-          camera_dir(k, rc, ddx, ddy, col, grow, ox, oy, oz, dx, dy, dz);
-          depth = 0;
-          thr = thg = thb = 1.0f;
-        }
-      } else {
-        alive = tracing = false;
-      }
-    }
+    // an absorbed path, or one at the bounce limit, parks its lane for a
+    // step: the lane takes its next item with the misses of the next step
+    // (one camera-ray path per step, with the step's one hash)
+    if (path_done) tracing = false;
     // one normalize3 per lane and step: the bounce direction or the new
     // camera ray's (a finished lane's is unused)
     if (alive) normalize3(dx, dy, dz);
