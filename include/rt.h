@@ -279,6 +279,12 @@ int rt_write_ppm(int fd, const uint8_t *rgb, int width, int height, int binary);
 enum { RT_KAT_SPHERE_HIT = 0, RT_KAT_REFLECT = 1, RT_KAT_REFRACT = 2, RT_KAT_REFLECTANCE = 3 };
 int rt_device_kat(int device, int kind, const double *in, size_t n_cases, double *out);
 
+/* Host only (no device): what rt_scene_upload would build for `scene` --
+ * BVH size, layer split, layer-grid dimensions, LDS footprint and the grid's
+ * invariants (cell i's items are [first_i, first_{i+1}); ring cells empty).
+ * out[16], layout in rt_render.hip.  For tests and sanitizer runs. */
+int rt_internal_accel_info(const rt_scene_view *scene, uint64_t *out);
+
 #ifdef __cplusplus
 }
 #endif

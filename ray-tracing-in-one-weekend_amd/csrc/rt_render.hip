@@ -164,9 +164,11 @@ typedef const __attribute__((address_space(3))) f4 lds_f4;
 __host__ __device__ constexpr size_t grid_lds_bytes(int n_items, int n_cells) {
   return (size_t)n_items * 16u + ((size_t)(n_cells + 1) * 2u + 15u) / 16u * 16u;
 }
-// LDS budget of the grid copy: 3 KB of static LDS + this stays within 20 KB
-// per 256-thread block, so 8 blocks (8 waves per SIMD) still fit in 160 KB
-constexpr size_t kGridLdsMax = 17 * 1024;
+// LDS budget of the grid copy: with render_kernel's static LDS (the tiles'
+// pixel sums and row indices) a 256-thread block stays within 20 KB, so 8
+// blocks (8 waves per SIMD) still fit in the CU's 160 KB
+constexpr size_t kStaticLds = 3 * kBlock * 4 + kWavesPerBlock * kTile * 4;
+constexpr size_t kGridLdsMax = 160 * 1024 / 8 - kStaticLds;
 
 // The kernel arguments, re-read from the kernarg segment (constant address
 // space: scalar loads that hit the scalar cache) at the rare places that need
@@ -2196,6 +2198,51 @@ int rt_render(rt_context *c, const rt_camera *cam, const rt_params *prm, float *
     if (st != RT_OK) return st;
     stats->kernel_ms = ms;
   }
+  return RT_OK;
+}
+
+// Host-only view of what rt_scene_upload would build (no device needed):
+// tests/test_host.py checks the builder's invariants on CPU, and
+// tools/host_sanitize.sh runs it under ASan / UBSan.  out[16]:
+//   0 nodes per DFS order   1 BVH slots          2 layer mode     3 extra_pair0
+//   4 n_extra_pairs         5 grid_nx (w/ ring)  6 grid_nz        7 grid items
+//   8 grid LDS bytes        9 grid fits the LDS 10 max items/cell 11 start invariant
+//  12 empty ring cells ok  13 oref * 1000      14 layer slots    15 listed cells
+int rt_internal_accel_info(const rt_scene_view *s, uint64_t *out) {
+  if (!s || !out) return RT_ERR_INVALID;
+  bvh_builder bb;
+  bb.run(s);
+  std::memset(out, 0, 16 * sizeof(uint64_t));
+  out[0] = bb.per_order;
+  out[1] = bb.slots.size();
+  out[2] = bb.layer_mode ? 1u : 0u;
+  out[3] = bb.extra_pair0;
+  out[4] = bb.n_extra_pairs;
+  out[5] = (uint64_t)bb.grid_nx;
+  out[6] = (uint64_t)bb.grid_nz;
+  const uint64_t items = bb.grid_items.size() / 4, cells = bb.grid_cells.size();
+  out[7] = items;
+  out[8] = cells ? rtk::grid_lds_bytes((int)items, (int)cells) : 0u;
+  out[9] = cells && items < 4096 && out[8] <= rtk::kGridLdsMax;
+  // every stored cell's first item is the running count (ring cells included),
+  // so cell i's items are [first_i, first_{i+1}) -- what the LDS walk reads
+  uint64_t maxc = 0, listed = 0;
+  bool start_ok = true, ring_ok = true;
+  for (uint64_t i = 0; i < cells; ++i) {
+    const uint32_t first = bb.grid_cells[i] >> 4, cnt = bb.grid_cells[i] & 15u;
+    const uint64_t next = i + 1 < cells ? (bb.grid_cells[i + 1] >> 4) : items;
+    start_ok = start_ok && first + cnt == next;
+    maxc = std::max<uint64_t>(maxc, cnt);
+    listed += cnt ? 1u : 0u;
+    const int a = (int)(i % bb.grid_nx), b = (int)(i / bb.grid_nx);
+    if (a == 0 || b == 0 || a == bb.grid_nx - 1 || b == bb.grid_nz - 1) ring_ok = ring_ok && cnt == 0;
+  }
+  out[10] = maxc;
+  out[11] = cells ? (start_ok ? 1u : 0u) : 0u;
+  out[12] = cells ? (ring_ok ? 1u : 0u) : 0u;
+  out[13] = (uint64_t)(bb.oref * 1000.0);
+  out[14] = bb.layer_mode ? (uint64_t)(2 * bb.extra_pair0) : 0u;
+  out[15] = listed;
   return RT_OK;
 }
 

@@ -123,6 +123,7 @@ def lib():
                                     ctypes.c_void_p]
         L.rt_write_ppm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_int]
+        L.rt_internal_accel_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -352,6 +353,21 @@ def device_kat(kind, cases, device=0):
     out = np.zeros((cases.shape[0], 9), np.float64)
     check(lib().rt_device_kat(device, kind, inp.ctypes.data, inp.shape[0], out.ctypes.data), "rt_device_kat")
     return out
+
+
+ACCEL_INFO_KEYS = ("nodes_per_order", "bvh_slots", "layer_mode", "extra_pair0", "n_extra_pairs",
+                   "grid_nx", "grid_nz", "grid_items", "grid_lds_bytes", "grid_fits_lds",
+                   "max_items_per_cell", "grid_starts_ok", "grid_ring_empty", "oref_milli",
+                   "layer_slots", "listed_cells")
+
+
+def accel_info(scene):
+    """What rt_scene_upload would build for `scene`, computed on the host
+    (rt_internal_accel_info; no device): a dict of ACCEL_INFO_KEYS."""
+    v = scene.view()
+    out = np.zeros(16, np.uint64)
+    check(lib().rt_internal_accel_info(ctypes.byref(v), out.ctypes.data), "rt_internal_accel_info")
+    return {k: int(x) for k, x in zip(ACCEL_INFO_KEYS, out)}
 
 
 def write_ppm(path, rgb, binary=False):

@@ -215,3 +215,34 @@ def test_cli_no_device_exit_99():
         pytest.skip("device present")
     r = subprocess.run([exe, "--spp", "1", "--quiet"], capture_output=True)
     assert r.returncode == 99  # src/gpu/cuda_utility.h:16
+
+
+def test_accel_builder_invariants_on_host(rtow):
+    """rt_internal_accel_info runs rt_scene_upload's BVH / layer-grid builder on
+    the host: the final scene is a layer scene whose grid fits the LDS budget of
+    8 blocks per CU; the 10 000-sphere scene's grid stays in global memory; the
+    five-sphere scene has no layer; every grid numbers its cells' first items by
+    the running count (cell i's items are [first_i, first_{i+1}), which the LDS
+    walk reads as two adjacent u16) and keeps its ring of cells empty."""
+    fin = rtow.accel_info(rtow.final_scene())
+    assert fin["layer_mode"] == 1 and fin["n_extra_pairs"] == 2
+    assert fin["grid_fits_lds"] == 1 and fin["grid_lds_bytes"] <= 160 * 1024 // 8 - 3200
+    assert fin["grid_starts_ok"] == 1 and fin["grid_ring_empty"] == 1
+    assert 1 <= fin["max_items_per_cell"] <= 15 and fin["grid_items"] >= 482
+    big = rtow.accel_info(rtow.final_scene(50))
+    assert big["layer_mode"] == 1 and big["grid_fits_lds"] == 0
+    assert big["grid_starts_ok"] == 1 and big["grid_ring_empty"] == 1
+    five = rtow.accel_info(rtow.five_scene())
+    assert five["layer_mode"] == 0 and five["grid_items"] == 0
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="needs hipcc")
+def test_host_code_under_asan_ubsan():
+    """tools/host_sanitize.sh: the scene builders, cameras, BVH / grid builder,
+    tonemaps and PPM writers under AddressSanitizer (with leak checks) and
+    UndefinedBehaviorSanitizer, host code only, no device."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([os.path.join(root, "tools", "host_sanitize.sh")], capture_output=True, text=True,
+                       timeout=900)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "host_sanitize: ok" in r.stdout
