@@ -1101,9 +1101,10 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
 // Several waves per tile (rt_params.units > 1): they added their integer pixel
 // sums into the frame (zeroed first), which holds uint32 sums until this pass
 // converts them in place, sum * 2^-F.  Memory-bound and tiny.
-__global__ __launch_bounds__(256) void finish_sums(float *__restrict__ out, uint64_t n, float qinv) {
+__global__ __launch_bounds__(256) void finish_sums(uint32_t *__restrict__ frame, uint64_t n, float qinv) {
+  // every access goes through the uint32 view: the float result is stored as its bits
   for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < n; j += (uint64_t)gridDim.x * 256u)
-    out[j] = (float)reinterpret_cast<const uint32_t *>(out)[j] * qinv;
+    frame[j] = __float_as_uint((float)frame[j] * qinv);
 }
 
 // Known-answer evaluation of the render kernel's own device arithmetic
@@ -2120,7 +2121,7 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
   RT_HIP(hipGetLastError());
   if (units > 1) {
     const unsigned grid = (unsigned)std::min<uint64_t>((frame_floats + 255) / 256, 256u * 64u);
-    rtk::finish_sums<<<grid, 256, 0, st>>>(accum_rgb, frame_floats, kp.qinv);
+    rtk::finish_sums<<<grid, 256, 0, st>>>(reinterpret_cast<uint32_t *>(accum_rgb), frame_floats, kp.qinv);
     RT_HIP(hipGetLastError());
   }
   RT_HIP(hipEventRecord(c->ev_done, st));
