@@ -810,7 +810,8 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
 }
 
 
-// 8 waves per SIMD (<= 64 VGPRs, 78 SGPRs).  The walk is a serial latency
+// 8 waves per SIMD (<= 64 VGPRs; the layer-grid build uses 61 VGPRs and 72
+// SGPRs, and 6 or 7 waves with more registers ran 2 % slower).  The walk is a serial latency
 // chain per wave (scalar node load -> slab test -> ballot -> branch), so more
 // resident waves keep the VALU busier: 312 vs 322 ms at 7 waves, although the
 // 8-wave budget spills a few per-step values (none inside the walk).  That
