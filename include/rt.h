@@ -135,9 +135,9 @@ typedef struct {
   int32_t band_offset;
   int32_t local_rows;
   uint32_t flags;
-  /* scheduling, not semantics: split every tile's samples (whole chunks of
-   * RT_CHUNK_SPP) over this many waves; 0 = choose from the tile count (1 for
-   * a 4K frame on one GPU, more when a rank's share of the frame is small) */
+  /* scheduling, not semantics: split every tile's samples into this many
+   * even shares, one wave each; 0 = choose from the tile count (1 for a 4K
+   * frame on one GPU, up to 8 when a rank's share of the frame is small) */
   uint32_t units;
 } rt_params;
 
@@ -145,8 +145,9 @@ typedef struct {
  * most 1: albedos must lie in [0, 1]) adds trunc(v * 2^F) to its pixel's
  * uint32 sum, F = 31 - floor(log2(spp)); the frame holds sum * 2^-F.  Integer
  * sums do not depend on the order, so samples can be traced by any lanes,
- * waves (rt_params.units, split in whole chunks of RT_CHUNK_SPP samples) or
- * GPUs without changing a single bit of the image. */
+ * waves (rt_params.units) or GPUs without changing a single bit of the
+ * image.  RT_CHUNK_SPP is kept for source compatibility (ABI 2 summed in
+ * chunks of 64 samples); nothing depends on it any more. */
 #define RT_CHUNK_SPP 64
 
 typedef struct {

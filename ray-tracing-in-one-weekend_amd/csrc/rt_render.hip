@@ -50,22 +50,25 @@ constexpr int kTile = 8;           // 8x8 pixels per wave
 constexpr int kWavesPerBlock = 4;  // 256 threads
 constexpr int kBlock = 64 * kWavesPerBlock;
 constexpr int kSpherePad = 8;      // scan unroll granularity
-// auto rt_params.units: below kSplitTiles tiles (86 016: 10.5 waves per wave
-// slot of the chip at 256 CUs x 4 SIMDs x 8) every chunk gets its own wave;
-// above it a wave traces all of its tile's samples.  Measured on the headline
-// frame (tools/rank_times.py, tools/units_frame.py): 1 GPU
-// (129 600 tiles) 302 ms unsplit vs 310 / 314 with units 2 / 4; a 1/2 share
-// (64 800 tiles) 175 ms unsplit vs 158 split, a 1/8 share 103 vs 42.
+// auto rt_params.units without the pilot schedule: below kSplitTiles tiles
+// (86 016: 10.5 waves per wave slot of the chip at 256 CUs x 4 SIMDs x 8) a
+// tile's samples are split over kUnits waves; above it a wave traces all of
+// them.  Measured on the headline frame before the sample pool (round 1,
+// tools/rank_times.py): 1 GPU (129 600 tiles) 302 ms unsplit vs
+// 310 / 314 with units 2 / 4; a 1/2 share (64 800 tiles) 175 ms unsplit vs
+// 158 split, a 1/8 share 103 vs 42.
 constexpr long long kSplitTiles = 12LL * 256 * 4 * 7;
 // With the pilot schedule (RT_FLAG_PILOT_SCHEDULE) the expensive tiles start
-// first, so the tail is short without splitting down to 6 waves per slot: a
-// 1/2 share (64 800 tiles) 151 ms unsplit vs 154 split, a 1/4 share (32 400)
-// 87 unsplit vs 78 split, 1/8 40 ms split (tools/rank_times.py --pilot).
-constexpr long long kSplitTilesPilot = 6LL * 256 * 4 * 8;
-// ... and, in pilot order, 4 waves per tile's chunks are enough: with the
-// layer grid a 1/4 share (32 400 tiles) runs 47.4 ms at units 4 vs 48.2 / 48.5
-// at 2 / 8, a 1/8 share 24.7 ms at 4 or 8 (29.7 at 2).
-constexpr int kPilotUnits = 4;
+// first, and with the sample pool a wave has no tail of its own, so the split
+// only needs ~16 waves per wave slot (8192 slots): units = round(131072 /
+// tiles), at most 8.  Measured with even sample shares (tools/rank_times.py
+// --pilot, tools/units_frame.py --pilot; profiles/r02zd_units_even_split.log):
+// the whole 4K frame (129 600 tiles) 142.8 ms unsplit; a 1/2 share 73.2 / 71.6
+// ms at units 1 / 2; a 1/4 share 39.2 / 36.7 / 36.0 at 1 / 2 / 4; a 1/8 share
+// 38.0 / 19.5 / 18.7 / 18.5 at 1 / 2 / 4 / 8; C1 (1080p, 100 spp, 32 400
+// tiles) 8.5 / 8.0 / 7.9 / 8.2 ms at 1 / 2 / 3 / 4.
+constexpr long long kPilotTilesPerUnit = 16LL * 256 * 4 * 8;
+constexpr int kUnits = 8;  // without the pilot
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -125,9 +128,9 @@ struct kparams {
   float inv_wm1, inv_hm1;  // 1/(W-1), 1/(H-1) rounded once (cpu camera model)
   // exact division by the width: W = wodd << wshift, wodd * winv == 1 (mod 2^32)
   uint32_t wshift, winv;
-  // sample chunks (RT_CHUNK_SPP) and their split over waves: block b traces
-  // chunks [u*cpu, (u+1)*cpu) of its tiles, u = b % units, cpu = chunks_per_unit
-  int units, chunks_per_unit;
+  // the split of a tile's samples over waves: block b traces samples
+  // [u spp / units, (u + 1) spp / units) of its tiles, u = b % units
+  int units, pad_u;
   // fixed-point pixel sums: a sample adds trunc(v 2^F)
   // to its pixel's uint32 sum; the frame holds sum 2^-F
   float qscale, qinv;  // 2^F, 2^-F with F = 31 - floor(log2(spp))
@@ -830,9 +833,9 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   const int unit = (int)(bid % (unsigned)p.units);
   const int tile = (int)(bid / (unsigned)p.units) * kWavesPerBlock + wave;
   const int col0 = (tile % p.tiles_x) * kTile, lrow0 = (tile / p.tiles_x) * kTile;
-  // this wave's samples: chunks [unit*cpu, (unit+1)*cpu) of RT_CHUNK_SPP each
-  const uint32_t s_begin = (uint32_t)(unit * p.chunks_per_unit) * RT_CHUNK_SPP;
-  const uint32_t s_end = min((uint32_t)((unit + 1) * p.chunks_per_unit) * RT_CHUNK_SPP, (uint32_t)p.spp);
+  // this wave's samples: an even share [unit spp / units, (unit + 1) spp / units)
+  const uint32_t s_begin = (uint32_t)((uint64_t)unit * (uint32_t)p.spp / (uint32_t)p.units);
+  const uint32_t s_end = (uint32_t)((uint64_t)(unit + 1) * (uint32_t)p.spp / (uint32_t)p.units);
   // The wave's work pool: item k of [0, kend) is sample
   // s_begin + k / 64 of the tile's pixel slot k % 64 (x = slot % 8, y = slot /
   // 8).  A lane whose path ends takes the next item, so no lane idles while
@@ -2044,23 +2047,22 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
                 ((prm->flags & RT_FLAG_COUNT_WORK) ? 8 : 0) |
                 ((c->d_grid_cells && !(prm->flags & RT_FLAG_LAYER_BVH)) ? 16 : 0) |
                 ((c->d_grid_cells && c->grid_lds && !(prm->flags & RT_FLAG_LAYER_BVH)) ? 32 : 0);
-  // sample chunks (RT_CHUNK_SPP) and how many waves share a tile's chunks.
-  // One wave per tile traces all of a pixel's samples in sequence; when a
-  // rank holds few tiles (a 1/8 share of a 4K frame is ~2.3 waves per wave
-  // slot), the slowest tiles (long glass / metal paths) then set the frame
-  // time, so the chunks are split over `units` waves (tools/rank_times.py).
-  const int n_chunks = std::max(1, (prm->spp + RT_CHUNK_SPP - 1) / RT_CHUNK_SPP);
+  // How many waves share a tile's samples (even shares; the integer pixel
+  // sums make any split give the same image).  One wave per tile traces all
+  // of its tile's samples; when a rank holds few tiles (a 1/8 share of a 4K
+  // frame is ~2 waves per wave slot), the slowest tiles (long glass / metal
+  // paths) then set the frame time, so the samples are split over `units`
+  // waves (tools/rank_times.py).
   long long units = prm->units;
   if (units <= 0) {
     const bool pilot = (prm->flags & RT_FLAG_PILOT_SCHEDULE) != 0;
-    units = tiles < (pilot ? rtk::kSplitTilesPilot : rtk::kSplitTiles) ? (pilot ? rtk::kPilotUnits : n_chunks) : 1;
+    units = pilot ? std::llround((double)rtk::kPilotTilesPerUnit / (double)std::max(1LL, tiles))
+                  : (tiles < rtk::kSplitTiles ? rtk::kUnits : 1);
+    units = std::min<long long>(std::max(units, 1LL), rtk::kUnits);
   }
   if (prm->spp <= 0 || prm->max_depth <= 0) units = 1;  // nothing is traced
-  units = std::max(1LL, std::min<long long>(units, n_chunks));
-  const int cpu = (int)((n_chunks + units - 1) / units);
-  units = (n_chunks + cpu - 1) / cpu;
+  units = std::max(1LL, std::min<long long>(units, prm->spp));  // >= 1 sample per unit
   kp.units = (int)units;
-  kp.chunks_per_unit = cpu;
   {
     int f = 31;  // F = 31 - floor(log2(spp)): spp samples of at most 2^F each fit a uint32
     for (int s = prm->spp; s > 1; s >>= 1) --f;
@@ -2094,7 +2096,6 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
         rtk::kparams pk = kp;
         pk.spp = std::min(prm->spp, 4);
         pk.units = 1;
-        pk.chunks_per_unit = 1;
         pk.tile_cost = d_cost;
         pk.counters = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(d_cost) + cost_bytes);
         kLaunch[(v & 55) | 8](blocks, st, pk, c, accum_rgb);

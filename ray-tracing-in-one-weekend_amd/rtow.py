@@ -34,7 +34,7 @@ RT_FLAG_ACCEL_BVH = 1 << 9
 RT_FLAG_COUNT_WORK = 1 << 10
 RT_FLAG_PILOT_SCHEDULE = 1 << 11  # launch expensive tiles first (4-spp pilot per frame geometry)
 RT_FLAG_LAYER_BVH = 1 << 12  # layer scenes: walk the layer BVH instead of the layer grid
-RT_CHUNK_SPP = 64  # include/rt.h: granularity of the units split (pixel sums are exact integers)
+RT_CHUNK_SPP = 64  # include/rt.h: kept for compatibility (pixel sums are exact integers, units split evenly)
 RT_TONEMAP_CPU, RT_TONEMAP_GPU = 0, 1  # write_color of src/cpu (fp64) / src/gpu (fp32)
 RT_KAT_SPHERE_HIT, RT_KAT_REFLECT, RT_KAT_REFRACT, RT_KAT_REFLECTANCE = 0, 1, 2, 3
 ABI_VERSION = 3
