@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--w", type=int, default=3840)
     ap.add_argument("--h", type=int, default=2160)
     ap.add_argument("--spp", type=int, default=500)
+    ap.add_argument("--pilot", action="store_true",
+                    help="RT_FLAG_PILOT_SCHEDULE: each value renders twice, the second (cached order) is timed")
     a = ap.parse_args()
     import rtow
     ctx = rtow.Context(0)
@@ -28,12 +30,14 @@ def main():
     cam = rtow.camera_cpu(aspect=a.w / a.h)
     ref = None
     for u in a.units:
-        p = rtow.make_params(a.w, a.h, a.spp, seed=0, flags=rtow.RT_FLAG_ACCEL_BVH)
+        flags = rtow.RT_FLAG_ACCEL_BVH | (rtow.RT_FLAG_PILOT_SCHEDULE if a.pilot else 0)
+        p = rtow.make_params(a.w, a.h, a.spp, seed=0, flags=flags)
         p.units = u
-        img, st = ctx.render(cam, p)
+        for _ in range(2 if a.pilot else 1):
+            img, st = ctx.render(cam, p)
         if ref is None:
             ref = img
-        print(json.dumps({"units": u, "kernel_ms": round(st.kernel_ms, 3),
+        print(json.dumps({"frame": f"{a.w}x{a.h}x{a.spp}", "pilot": a.pilot, "units": u, "kernel_ms": round(st.kernel_ms, 3),
                           "identical": bool(np.array_equal(ref, img))}), flush=True)
 
 
