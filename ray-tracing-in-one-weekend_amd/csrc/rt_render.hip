@@ -1792,6 +1792,25 @@ hipError_t upload_vec(T **dst, const std::vector<T> &v, hipStream_t st) {
 
 }  // namespace
 
+// What rt_scene_upload (and rt_internal_accel_info) accept: arrays present,
+// known materials, finite centres and radii, non-zero radii, and albedos in
+// [0, 1] (energy-conserving materials: a sample's radiance is then at most 1,
+// which the fixed-point pixel sums rely on; dielectrics
+// ignore theirs).  The builder's sorts need finite keys.
+static bool scene_ok(const rt_scene_view *s) {
+  if (!s || (s->n && (!s->cx || !s->cy || !s->cz || !s->radius || !s->mat_kind || !s->mat_param ||
+                      !s->albedo_rgb)))
+    return false;
+  for (uint32_t i = 0; i < s->n; ++i) {
+    if (s->mat_kind[i] > RT_DIELECTRIC || !(s->radius[i] != 0.0f) || !std::isfinite(s->radius[i]) ||
+        !std::isfinite(s->cx[i]) || !std::isfinite(s->cy[i]) || !std::isfinite(s->cz[i]))
+      return false;
+    for (int k = 0; k < 3 && s->mat_kind[i] != RT_DIELECTRIC; ++k)
+      if (!(s->albedo_rgb[3 * i + k] >= 0.0f && s->albedo_rgb[3 * i + k] <= 1.0f)) return false;
+  }
+  return true;
+}
+
 extern "C" {
 
 int rt_device_count(int *count) {
@@ -1860,19 +1879,7 @@ void rt_context_destroy(rt_context *c) {
 }
 
 int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
-  if (!c || !s || (s->n && (!s->cx || !s->cy || !s->cz || !s->radius || !s->mat_kind ||
-                            !s->mat_param || !s->albedo_rgb)))
-    return RT_ERR_INVALID;
-  for (uint32_t i = 0; i < s->n; ++i)
-    if (s->mat_kind[i] > RT_DIELECTRIC || !(s->radius[i] != 0.0f) || !std::isfinite(s->radius[i]) ||
-        !std::isfinite(s->cx[i]) || !std::isfinite(s->cy[i]) || !std::isfinite(s->cz[i]))
-      return RT_ERR_INVALID;
-  // albedos in [0, 1] (energy-conserving materials): a sample's radiance is
-  // then at most 1, which the fixed-point pixel sums rely on (DESIGN.md 2,
-  // step 6); dielectrics ignore theirs
-  for (uint32_t i = 0; i < s->n; ++i)
-    for (int k = 0; k < 3 && s->mat_kind[i] != RT_DIELECTRIC; ++k)
-      if (!(s->albedo_rgb[3 * i + k] >= 0.0f && s->albedo_rgb[3 * i + k] <= 1.0f)) return RT_ERR_INVALID;
+  if (!c || !scene_ok(s)) return RT_ERR_INVALID;
   const uint32_t n = s->n;
   const uint32_t n_pad = (n + rtk::kSpherePad - 1) / rtk::kSpherePad * rtk::kSpherePad;
   std::vector<rtk::pair_geom> geom(n_pad / 2);
@@ -2212,7 +2219,7 @@ int rt_render(rt_context *c, const rt_camera *cam, const rt_params *prm, float *
 //   8 grid LDS bytes        9 grid fits the LDS 10 max items/cell 11 start invariant
 //  12 empty ring cells ok  13 oref * 1000      14 layer slots    15 listed cells
 int rt_internal_accel_info(const rt_scene_view *s, uint64_t *out) {
-  if (!s || !out) return RT_ERR_INVALID;
+  if (!out || !scene_ok(s)) return RT_ERR_INVALID;
   bvh_builder bb;
   bb.run(s);
   std::memset(out, 0, 16 * sizeof(uint64_t));

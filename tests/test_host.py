@@ -246,3 +246,33 @@ def test_host_code_under_asan_ubsan():
                        timeout=900)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "host_sanitize: ok" in r.stdout
+
+
+def test_scene_validation_on_host(rtow):
+    """rt_scene_upload's validation (shared with rt_internal_accel_info, so it
+    runs without a device): non-finite centres, zero radii, unknown materials
+    and lambertian / metal albedos outside [0, 1] are RT_ERR_INVALID; a
+    dielectric's albedo is ignored."""
+    import dataclasses
+    base = rtow.final_scene()
+    assert rtow.accel_info(base)["layer_mode"] == 1
+    lam = int(np.nonzero(base.kind == rtow.RT_LAMBERTIAN)[0][0])
+    met = int(np.nonzero(base.kind == rtow.RT_METAL)[0][0])
+    die = int(np.nonzero(base.kind == rtow.RT_DIELECTRIC)[0][0])
+
+    def with_(name, i, value, col=None):
+        a = getattr(base, name).copy()
+        if col is None:
+            a[i] = value
+        else:
+            a[i, col] = value
+        return dataclasses.replace(base, **{name: a})
+
+    bad = [with_("cx", 5, float("nan")), with_("cz", 5, float("inf")), with_("radius", 5, 0.0),
+           with_("kind", 5, 7), with_("albedo", lam, 1.5, 0), with_("albedo", met, -0.1, 2),
+           with_("albedo", lam, float("nan"), 1)]
+    for sc in bad:
+        with pytest.raises(rtow.RTError) as ei:
+            rtow.accel_info(sc)
+        assert ei.value.status == rtow.RT_ERR_INVALID
+    assert rtow.accel_info(with_("albedo", die, 9.0, 0))["layer_mode"] == 1
