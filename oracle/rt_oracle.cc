@@ -22,6 +22,7 @@
 //
 // Reference anchors are cited per function (paths under /root/reference).
 #include "rt_oracle.h"
+#include "rt_turn_table.h"
 
 #include <algorithm>
 #include <atomic>
@@ -289,28 +290,27 @@ u4 pcg4d(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
 
 inline float unif(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
 
+// the kernel's sin/cos of 2 pi u (rt_render.hip sincos_turn): the (cos, sin)
+// table of include/rt_turn_table.h at i = floor(1024 u), rotated by the
+// remainder d with cos d = 1 - d^2/2, sin d = d (1 - d^2/6)
+const float *turn_table() {
+  static const std::vector<float> tab = [] {
+    std::vector<float> t(2 * RT_TURN_TABLE);
+    rt_turn_table(t.data());
+    return t;
+  }();
+  return tab.data();
+}
 void sincos_turn(float u, float &s, float &c) {
-  float q4 = u * 4.0f;
-  float qf = std::floor(q4);
-  int q = (int)qf;
-  float x = (q4 - qf) * 1.57079632679489662f;
-  float x2 = x * x;
-  float sp = fmaf_(x2, -2.50521084e-08f, 2.75573192e-06f);
-  sp = fmaf_(x2, sp, -1.98412698e-04f);
-  sp = fmaf_(x2, sp, 8.33333333e-03f);
-  sp = fmaf_(x2, sp, -1.66666667e-01f);
-  sp = fmaf_(x2, sp, 1.0f);
-  float sn = x * sp;
-  float cp = fmaf_(x2, 2.08767570e-09f, -2.75573192e-07f);
-  cp = fmaf_(x2, cp, 2.48015873e-05f);
-  cp = fmaf_(x2, cp, -1.38888889e-03f);
-  cp = fmaf_(x2, cp, 4.16666667e-02f);
-  cp = fmaf_(x2, cp, -0.5f);
-  float cs = fmaf_(x2, cp, 1.0f);
-  float s0 = (q & 1) ? cs : sn;
-  float c0 = (q & 1) ? sn : cs;
-  s = (q & 2) ? -s0 : s0;
-  c = ((q + 1) & 2) ? -c0 : c0;
+  const float t = u * (float)RT_TURN_TABLE;
+  const float fl = std::floor(t);
+  const float *e = turn_table() + 2 * (int)fl;
+  const float d = (t - fl) * (6.28318530717958648f / (float)RT_TURN_TABLE);
+  const float x2 = d * d;
+  const float cd = fmaf_(x2, -0.5f, 1.0f);
+  const float sd = d * fmaf_(x2, -0.166666667f, 1.0f);
+  c = fmaf_(e[0], cd, -(e[1] * sd));
+  s = fmaf_(e[1], cd, e[0] * sd);
 }
 
 // the kernel's radius of a uniform point in the unit ball (radius law of

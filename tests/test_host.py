@@ -276,3 +276,43 @@ def test_scene_validation_on_host(rtow):
             rtow.accel_info(sc)
         assert ei.value.status == rtow.RT_ERR_INVALID
     assert rtow.accel_info(with_("albedo", die, 9.0, 0))["layer_mode"] == 1
+
+
+def test_turn_table_deterministic_and_accurate(tmp_path):
+    """include/rt_turn_table.h (the kernel's and the oracle's sin/cos table):
+    the same bits from gcc and from a restatement in Python doubles (the
+    series uses only IEEE double arithmetic), and within 1 fp32 ulp of cos /
+    sin of 2 pi i / 1024."""
+    src = tmp_path / "t.c"
+    src.write_text('#include <stdio.h>\n#include "rt_turn_table.h"\n'
+                   'int main(void) { static float t[2 * RT_TURN_TABLE]; rt_turn_table(t);\n'
+                   '  fwrite(t, sizeof t, 1, stdout); return 0; }\n')
+    exe = tmp_path / "t"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-I", os.path.join(ROOT, "include"), "-o", str(exe),
+                    str(src)], check=True)
+    got = np.frombuffer(subprocess.run([str(exe)], capture_output=True, check=True).stdout,
+                        dtype=np.float32).reshape(-1, 2)
+    n = 1024
+    assert got.shape == (n, 2)
+    want = np.empty((n, 2), np.float32)
+    for i in range(n):
+        x = 6.283185307179586476925 * float(i % (n // 4)) / float(n)
+        c = s = 0.0
+        term = 1.0
+        for k in range(32):
+            if k % 4 == 0:
+                c += term
+            elif k % 4 == 1:
+                s += term
+            elif k % 4 == 2:
+                c -= term
+            else:
+                s -= term
+            term = term * x / float(k + 1)
+        fc, fs = np.float32(c), np.float32(s)
+        want[i] = [(fc, fs), (-fs, fc), (-fc, -fs), (fs, -fc)][i // (n // 4)]
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    a = 2.0 * np.pi * np.arange(n) / n
+    exact = np.stack([np.cos(a), np.sin(a)], axis=1)
+    ulp = np.spacing(np.abs(exact).astype(np.float32)).astype(np.float64)
+    assert np.all(np.abs(got.astype(np.float64) - exact) <= np.maximum(ulp, 1e-15))  # exact zeros where cos / sin vanish
