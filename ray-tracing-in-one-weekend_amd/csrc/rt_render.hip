@@ -241,27 +241,21 @@ __device__ __forceinline__ uint4 pcg4d(uint32_t a, uint32_t b, uint32_t c, uint3
 
 __device__ __forceinline__ float unif(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
 
-// sqrtf(max(x, 2^-96)), correctly rounded.  v_sqrt_f32 is within 1 ulp; the
-// two fma residuals pick the correctly rounded neighbour (LLVM's own expansion
-// of sqrtf).  Clamping the argument to >= 2^-96 removes the expansion's
-// denormal-range rescaling and its inf/nan fix-up: 10 VALU instead of 17.  No
-// call site can tell the clamp from sqrtf (arguments are 0 or >> 2^-96, and a
-// root 2^-48 instead of 0 rounds away against any t >= 0.001); the host
-// restatement applies the same clamp anyway.
-// sqrt_nc: the same without the clamp, for the candidate roots h -+ sq only
-// (x >= 0 there).  An argument below 2^-96 gives some sq < 2^-48 instead of
-// 2^-48: if |h| >= 2^-20 both round h -+ sq to h, and otherwise t1 < t_min
-// rejects the sphere either way -- the same outcome as sqrt_k, one VALU less
-// per candidate sequence (the host restatement keeps the clamp).
-__device__ __forceinline__ float sqrt_nc(float x) {
-  const float y = __builtin_amdgcn_sqrtf(x);
-  const float ydn = __uint_as_float(__float_as_uint(y) - 1u);
-  const float yup = __uint_as_float(__float_as_uint(y) + 1u);
-  float r = (fmaf(-ydn, y, x) <= 0.0f) ? ydn : y;
-  r = (fmaf(-yup, y, x) > 0.0f) ? yup : r;
-  return r;
+// sqrtf(max(x, 2^-96)), correctly rounded: y = v_rsq_f32(x), s = x y, then one
+// Newton step on the product, s + (x - s^2) y/2.  Equal to the correctly
+// rounded sqrt for every fp32 in [2^-96, +inf) (checked exhaustively on the
+// GPU: tools/ubench_sqrt2.hip, profiles/r02zh_ubench_sqrt2.log); below 2^-96
+// it is not (NaN at 0), and the clamp keeps those out.  5 VALU + the clamp,
+// against 9 for v_sqrt_f32 with LLVM's two-residual correction, at 2.3x its
+// issue rate.  No call site can tell the clamp from sqrtf (arguments are 0 or
+// >> 2^-96, and a root 2^-48 instead of 0 rounds away against any t >=
+// 0.001); the host restatement applies the same clamp.
+__device__ __forceinline__ float sqrt_k(float x) {
+  x = fmaxf(x, 0x1p-96f);
+  const float y = __builtin_amdgcn_rsqf(x);
+  const float s = x * y, hy = 0.5f * y;
+  return fmaf(fmaf(-s, s, x), hy, s);
 }
-__device__ __forceinline__ float sqrt_k(float x) { return sqrt_nc(fmaxf(x, 0x1p-96f)); }
 
 // sin/cos of 2 pi u, u in [0, 1): the table's (cos, sin) of 2 pi i / 1024 for
 // i = floor(1024 u) (include/rt_turn_table.h: fp64 Taylor, rounded once; the
@@ -448,7 +442,7 @@ __device__ __forceinline__ hit_state no_hit() { return hit_state{__builtin_huge_
 template <bool OPEN>
 __device__ __forceinline__ void candidate(bool c, float h, float disc, uint32_t tie2, hit_state &hs) {
   if (c) {
-    const float sq = sqrt_nc(disc);
+    const float sq = sqrt_k(disc);
     const float t0 = h - sq, t1 = h + sq;
     const bool use0 = OPEN ? (t0 > 0.001f) : (t0 >= 0.001f);
     const float root = use0 ? t0 : t1;

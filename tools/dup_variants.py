@@ -31,28 +31,22 @@ EDITS = {
     "extras": [("      if (STATS) wc.tests += 2 * p.n_extra_pairs;",
                 """      if (STATS) wc.tests += 2 * p.n_extra_pairs;
       {
-        hit_state h2{__builtin_huge_valf(), -1, 1};
+        hit_state h2 = no_hit();
         ray_pre r2 = rp;
         asm volatile("" : "+v"(r2.dx), "+v"(r2.nk1));
         for (int k = 0; k < p.n_extra_pairs; k += 2)
           scan_pairs<OPEN, 2, STATS>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, r2, h2, wc.roots);
-        asm volatile("" :: "v"(h2.tmax), "v"(h2.best));
+        asm volatile("" :: "v"(h2.tmax), "v"(h2.lo));
       }""")],
-    # the correctly rounded sqrt of each candidate sphere
-    "rootsqrt": [("    const float sq = sqrt_k(disc);\n    const float t0 = h - sq, t1 = h + sq;",
-                  """    const float sq = sqrt_k(disc);
-    float dd = disc;
-    asm volatile("" : "+v"(dd));
-    const float sq2 = sqrt_k(dd);
-    asm volatile("" :: "v"(sq2));
-    const float t0 = h - sq, t1 = h + sq;""")],
-    # the bounce's pcg4d
-    "pcg": [("      const uint4 r = pcg4d(pix, miss ? sample : sample - 1u, miss ? 0u : (uint32_t)(depth + 1), q.seed32);",
-             """      const uint4 r = pcg4d(pix, miss ? sample : sample - 1u, miss ? 0u : (uint32_t)(depth + 1), q.seed32);
-      uint32_t pq = pix;
-      asm volatile("" : "+v"(pq));
-      const uint4 r2 = pcg4d(pq, miss ? sample : sample - 1u, miss ? 0u : (uint32_t)(depth + 1), q.seed32);
-        asm volatile("" :: "v"(r2.x), "v"(r2.y), "v"(r2.z));""")],
+    # the bounce's / camera ray's pcg4d (one per lane and step)
+    "pcg": [("      const uint4 r = pcg4d(pix, sample, miss ? 0u : (uint32_t)(depth + 1), q.seed32);",
+             """      const uint4 r = pcg4d(pix, sample, miss ? 0u : (uint32_t)(depth + 1), q.seed32);
+      {
+        uint32_t pq = pix;
+        asm volatile("" : "+v"(pq));
+        const uint4 r2 = pcg4d(pq, sample, miss ? 0u : (uint32_t)(depth + 1), q.seed32);
+        asm volatile("" :: "v"(r2.x), "v"(r2.y), "v"(r2.z), "v"(r2.w));
+      }""")],
     # the per-step polar draw (sqrt + sin/cos)
     "sincos": [("  sincos_turn(u, s, c);\n  x = rho * c;",
                 """  sincos_turn(u, s, c);
@@ -69,36 +63,49 @@ EDITS = {
         const float t2 = refine_root(sr, tq, near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2, b2);
         asm volatile("" :: "v"(t2), "v"(b2));""")],
     # the whole layer-grid walk (DDA + cell items + candidates), a second time
-    "gridwalk": [("        if (tyl_n <= tyl_fc) grid_walk<OPEN, STATS>(ox, oz, ix, iz, oix, oiz, tyl_n, tyl_fc, rg, hs, wc);",
+    "gridwalk": [("        if (tyl_n <= tyl_fc) grid_walk<OPEN, STATS, GLDS>(ox, oz, ix, iz, oix, oiz, tyl_n, tyl_fc, rg, hs, wc);",
                   """        if (tyl_n <= tyl_fc) {
           hit_state h2 = hs;
           float ta2 = tyl_n;
           asm volatile("" : "+v"(ta2), "+v"(h2.tmax));
-          grid_walk<OPEN, STATS>(ox, oz, ix, iz, oix, oiz, ta2, tyl_fc, rg, h2, wc);
-          asm volatile("" :: "v"(h2.tmax), "v"(h2.best), "v"(h2.near));
+          grid_walk<OPEN, STATS, GLDS>(ox, oz, ix, iz, oix, oiz, ta2, tyl_fc, rg, h2, wc);
+          asm volatile("" :: "v"(h2.tmax), "v"(h2.lo));
         }
-        if (tyl_n <= tyl_fc) grid_walk<OPEN, STATS>(ox, oz, ix, iz, oix, oiz, tyl_n, tyl_fc, rg, hs, wc);""")],
-    # the grid walk's item loads (16 B per lane from L1)
-    "itemload": [("      const f4 it = items[first + k];",
-                  """      const f4 it = items[first + k];
+        if (tyl_n <= tyl_fc) grid_walk<OPEN, STATS, GLDS>(ox, oz, ix, iz, oix, oiz, tyl_n, tyl_fc, rg, hs, wc);""")],
+    # the grid walk's item loads (16 B per lane from LDS)
+    "itemload": [("      const f4 it = GLDS ? *ip : items[first + k];",
+                  """      const f4 it = GLDS ? *ip : items[first + k];
       {
-        uint32_t kk = first + k;
-        asm volatile("" : "+v"(kk));
-        const f4 it2 = items[kk];
+        lds_f4 *ip2 = ip;
+        asm volatile("" : "+v"(ip2));
+        const f4 it2 = *ip2;
         asm volatile("" :: "v"(it2.x), "v"(it2.y), "v"(it2.z), "v"(it2.w));
       }""")],
-    # the grid walk's cell loads (4 B per lane)
-    "cellload": [("    const uint32_t ce = cells[(uint32_t)cell];",
-                  """    const uint32_t ce = cells[(uint32_t)cell];
-    {
-      uint32_t c2 = (uint32_t)cell;
+    # the grid walk's item test (load + 5 fma + compare), without the candidate
+    "itemtest": [("      const f4 it = GLDS ? *ip : items[first + k];",
+                  """      const f4 it = GLDS ? *ip : items[first + k];
+      {
+        lds_f4 *ip2 = ip;
+        asm volatile("" : "+v"(ip2));
+        const f4 i2 = *ip2;
+        const float h2 = fmaf(i2.y, dz, fmaf(i2.x, dx, rl.nk1.x));
+        const float g2 = fmaf(i2.y, rl.oz2.x, fmaf(i2.x, rl.ox2.x, rl.o2.x));
+        const float e2 = fmaf(h2, h2, -g2);
+        const uint64_t m2 = __builtin_amdgcn_ballot_w64(e2 >= i2.z);
+        asm volatile("" :: "s"(m2));
+      }""")],
+    # the grid walk's cell loads (two ds_read_u16 per cell)
+    "cellload": [("    if (GLDS) asm volatile(\"\" : \"+v\"(ie));",
+                  """    if (GLDS) asm volatile("" : "+v"(ie));
+    if (GLDS) {
+      int c2 = cell;
       asm volatile("" : "+v"(c2));
-      const uint32_t ce2 = cells[c2];
-      asm volatile("" :: "v"(ce2));
+      const uint32_t a2 = ((lds_u16 *)(uintptr_t)c2)[0], b2 = ((lds_u16 *)(uintptr_t)c2)[1];
+      asm volatile("" :: "v"(a2), "v"(b2));
     }""")],
     # every candidate's root / interval sequence (sqrt, roots, tie rule)
-    "candidate": [("template <bool OPEN>\n__device__ __forceinline__ void candidate(bool c, float h, float disc, int idx, hit_state &hs) {\n  if (c) {",
-                   """template <bool OPEN>\n__device__ __forceinline__ void candidate(bool c, float h, float disc, int idx, hit_state &hs) {\n  if (c) {
+    "candidate": [("__device__ __forceinline__ void candidate(bool c, float h, float disc, uint32_t tie2, hit_state &hs) {\n  if (c) {",
+                   """__device__ __forceinline__ void candidate(bool c, float h, float disc, uint32_t tie2, hit_state &hs) {\n  if (c) {
     {
       float h2 = h, d2 = disc;
       asm volatile("" : "+v"(h2), "+v"(d2));
@@ -106,21 +113,32 @@ EDITS = {
       const float a0 = h2 - sq2, a1 = h2 + sq2;
       const bool u0 = OPEN ? (a0 > 0.001f) : (a0 >= 0.001f);
       const float rt = u0 ? a0 : a1;
-      const bool ab = OPEN ? (rt > 0.001f) : (rt >= 0.001f);
-      const bool cl = (rt < hs.tmax) | ((rt == hs.tmax) & (OPEN ? (idx < hs.best) : (idx > hs.best)));
-      float o = (ab & cl) ? rt : 0.0f;
+      const bool ab = OPEN ? (a1 > 0.001f) : (a1 >= 0.001f);
+      const uint32_t lo2 = tie2 + (u0 ? 1u : 0u);
+      const uint64_t k2 = ((uint64_t)__float_as_uint(rt) << 32) | lo2;
+      const uint64_t c2 = ((uint64_t)__float_as_uint(hs.tmax) << 32) | hs.lo;
+      float o = (ab & (k2 < c2)) ? rt : 0.0f;
       asm volatile("" :: "v"(o));
     }""")],
-    # the camera direction of the next sample (path regeneration)
-    "camera": [("          camera_dir(k, rc, ddx, ddy, col, grow, ox, oy, oz, dx, dy, dz);",
-                """          camera_dir(k, rc, ddx, ddy, col, grow, ox, oy, oz, dx, dy, dz);
-          {
-            uint4 r2 = rc;
-            asm volatile("" : "+v"(r2.x), "+v"(r2.y), "+v"(r2.z), "+v"(r2.w));
-            float a0, a1, a2, a3, a4, a5;
-            camera_dir(k, r2, ddx, ddy, col, grow, a0, a1, a2, a3, a4, a5);
-            asm volatile("" :: "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5));
-          }""")],
+    # the camera direction of a new item (path regeneration)
+    "camera": [("        camera_dir(q, r, ux, uy, col, grow, ox, oy, oz, dx, dy, dz);",
+                """        camera_dir(q, r, ux, uy, col, grow, ox, oy, oz, dx, dy, dz);
+        {
+          uint4 r2 = r;
+          asm volatile("" : "+v"(r2.x), "+v"(r2.y), "+v"(r2.z), "+v"(r2.w));
+          float a0, a1, a2, a3, a4, a5;
+          camera_dir(q, r2, ux, uy, col, grow, a0, a1, a2, a3, a4, a5);
+          asm volatile("" :: "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5));
+        }""")],
+    # the per-step normalisation of the new direction
+    "normalize": [("    if (alive) normalize3(dx, dy, dz);",
+                   """    if (alive) {
+      float x2 = dx, y2 = dy, z2 = dz;
+      asm volatile("" : "+v"(x2), "+v"(y2), "+v"(z2));
+      normalize3(x2, y2, z2);
+      asm volatile("" :: "v"(x2), "v"(y2), "v"(z2));
+    }
+    if (alive) normalize3(dx, dy, dz);""")],
     # the material scatter (all three branches as the wave runs them)
 }
 
