@@ -22,7 +22,7 @@ import numpy as np
 import pytest
 
 from oracle_lib import golden_kat, golden_ppm, golden_stats, kernel_render, read_ppm_bytes
-from test_oracle import block_means
+from test_oracle import IMAGE22, block_means, blocks8, gallery_compare, image22_camera
 
 pytestmark = pytest.mark.gpu
 
@@ -123,6 +123,23 @@ def test_five_scene_gpu_camera_defocus_bit_exact(rtow, gpu_ctx, oracle, flags):
     got, st = gpu_ctx.render(cam, p)
     assert np.array_equal(got, want), int((got != want).sum())
     assert st.segments == segs
+
+
+def test_gpu_semantics_vs_reference_gpu_gallery_image22(rtow, gpu_ctx):
+    """The product with src/gpu's semantics (RT_FLAG_GPU_SEMANTICS, src/gpu
+    camera with image22's defocus, device fp32 write_color) against the
+    reference CUDA path's own output, gallery/gpu/image22.png: 1920x1080 at 10
+    spp, two seeds for the noise floor (bounds in test_oracle.gallery_compare)."""
+    gpu_ctx.upload(rtow.five_scene())
+    cam = image22_camera(rtow)
+    blk = []
+    for seed in (1, 2):
+        p = rtow.make_params(IMAGE22["width"], IMAGE22["height"], IMAGE22["spp"], seed=seed,
+                             flags=GRID | rtow.RT_FLAG_GPU_SEMANTICS)
+        sums, _ = gpu_ctx.render(cam, p)
+        img = device_tonemap(rtow, gpu_ctx, sums, IMAGE22["spp"], rtow.RT_TONEMAP_GPU)
+        blk.append(blocks8(img))
+    print("image22", gallery_compare(*blk))
 
 
 # ------------------------------------------------------------ write_color --
