@@ -91,6 +91,14 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; "
                                "g.build()'` (or make -C ray-tracing-in-one-weekend_amd)")
+        # torch's bundled HIP runtime has the same soname as the system one
+        # librtow links (libamdhip64.so.7): whichever loads first serves the
+        # process, and torch cannot enumerate devices through the system's.
+        # So torch, when present, loads first ("Loading").
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         d3 = ctypes.POINTER(ctypes.c_double)
         L.rt_abi_version.restype = ctypes.c_int
