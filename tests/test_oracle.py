@@ -161,18 +161,23 @@ def test_kernel_mode_depth_zero_and_spp_zero(rtow):
 # ------------------------------------------- the reference's own GPU output --
 
 IMAGE22 = dict(width=1920, height=1080, spp=10)
+# archive-gpu/imageN/camera.h: vfov, defocus angle (image20/21 have no lens:
+# focal length |lookfrom - lookat| = sqrt(12), which scales the viewport only)
+GALLERY = {"image20": (90.0, 0.0, 12 ** 0.5), "image21": (20.0, 0.0, 12 ** 0.5), "image22": (20.0, 10.0, 3.4)}
 
 
-def image22_camera(rtow):
-    """archive-gpu/image22/camera.h:58-71: src/gpu's camera model, vfov 20,
-    lookfrom (-2, 2, 1), lookat (0, 0, -1), defocus 10 deg at focus 3.4."""
+def image22_camera(rtow, name="image22"):
+    """archive-gpu/image20..22/camera.h: src/gpu's camera model, lookfrom
+    (-2, 2, 1), lookat (0, 0, -1); image22: vfov 20, defocus 10 deg at focus
+    3.4 (camera.h:58-71)."""
+    vfov, defocus, focus = GALLERY[name]
     return rtow.camera_gpu(IMAGE22["width"], IMAGE22["height"], lookfrom=(-2, 2, 1), lookat=(0, 0, -1),
-                           vfov=20.0, defocus_angle=10.0, focus_dist=3.4)
+                           vfov=vfov, defocus_angle=defocus, focus_dist=focus)
 
 
-def gallery_image22_blocks():
-    """8x8 block means of gallery/gpu/image22.png (tests/golden/make_gallery_fixture.py)."""
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "gallery_gpu_image22_blocksum8.npz")
+def gallery_blocks(name):
+    """8x8 block means of gallery/gpu/<name>.png (tests/golden/make_gallery_fixture.py)."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"gallery_gpu_{name}_blocksum8.npz")
     return np.load(path)["blocksum8"].astype(np.float64) / 64.0
 
 
@@ -181,16 +186,16 @@ def blocks8(img_u8):
     return img_u8.reshape(h // 8, 8, w // 8, 8, 3).astype(np.float64).mean(axis=(1, 3))
 
 
-def gallery_compare(a, b):
+def gallery_compare(a, b, name="image22"):
     """Two renders of ours (block means a, b: different seeds) against the
     reference CUDA path's image (one curand stream per pixel, its own seed).
     Bounds: 8x8 block-mean error <= 1.1 x our own seed-to-seed floor, and
     image-mean bias per channel <= max(4 sigma, 0.1 level).  The reference's
-    image is ~0.05 level darker in red and green than ours (5 sigma at 2 M
+    image22 is ~0.05 level darker in red and green than ours (5 sigma at 2 M
     pixels), most likely the grazing rays its fp32 quadratic traps and the
     refined roots do not; 0.1 level is a tenth of
     north_star's 1/255."""
-    g = gallery_image22_blocks()
+    g = gallery_blocks(name)
     n = a.shape[0] * a.shape[1]
     sigma = (a - b).reshape(-1, 3).std(0) / np.sqrt(n)
     bias = a.reshape(-1, 3).mean(0) - g.reshape(-1, 3).mean(0)
@@ -203,18 +208,19 @@ def gallery_compare(a, b):
     return report
 
 
-def test_kernel_gpu_semantics_matches_reference_gpu_gallery_image22(rtow):
+@pytest.mark.parametrize("name", sorted(GALLERY))
+def test_kernel_gpu_semantics_matches_reference_gpu_gallery(rtow, name):
     """The oracle's kernel mode with src/gpu's semantics (open interval, fuzz x
-    unit vector, src/gpu camera with defocus, fp32 write_color) against the one
-    output of the reference's CUDA path that is reproducible:
-    gallery/gpu/image22.png, the five-sphere scene at 1920x1080 and 10 spp
-    (parity for the gpu_ray_tracer personality)."""
+    unit vector, src/gpu camera, fp32 write_color) against the outputs of the
+    reference's CUDA path that are reproducible: gallery/gpu/image20..22.png,
+    the five-sphere scene at 1920x1080 and 10 spp, three cameras (parity for
+    the gpu_ray_tracer personality)."""
     scene = rtow.five_scene()
-    cam = image22_camera(rtow)
+    cam = image22_camera(rtow, name)
     blk = []
     for seed in (1, 2):
         p = rtow.make_params(IMAGE22["width"], IMAGE22["height"], IMAGE22["spp"], seed=seed,
                              flags=rtow.RT_FLAG_GPU_SEMANTICS)
         sums, _ = kernel_render(scene, cam, p, threads=8)
         blk.append(blocks8(rtow.tonemap(sums, IMAGE22["spp"], rtow.RT_TONEMAP_GPU)))
-    print(gallery_compare(*blk))
+    print(name, gallery_compare(*blk, name=name))

@@ -125,13 +125,15 @@ def test_five_scene_gpu_camera_defocus_bit_exact(rtow, gpu_ctx, oracle, flags):
     assert st.segments == segs
 
 
-def test_gpu_semantics_vs_reference_gpu_gallery_image22(rtow, gpu_ctx):
+@pytest.mark.parametrize("name", ["image20", "image21", "image22"])
+def test_gpu_semantics_vs_reference_gpu_gallery(rtow, gpu_ctx, name):
     """The product with src/gpu's semantics (RT_FLAG_GPU_SEMANTICS, src/gpu
-    camera with image22's defocus, device fp32 write_color) against the
-    reference CUDA path's own output, gallery/gpu/image22.png: 1920x1080 at 10
-    spp, two seeds for the noise floor (bounds in test_oracle.gallery_compare)."""
+    camera, device fp32 write_color) against the reference CUDA path's own
+    outputs, gallery/gpu/image20..22.png: the five-sphere scene at 1920x1080
+    and 10 spp through three cameras (image22 with depth of field); two seeds
+    for the noise floor (bounds in test_oracle.gallery_compare)."""
     gpu_ctx.upload(rtow.five_scene())
-    cam = image22_camera(rtow)
+    cam = image22_camera(rtow, name)
     blk = []
     for seed in (1, 2):
         p = rtow.make_params(IMAGE22["width"], IMAGE22["height"], IMAGE22["spp"], seed=seed,
@@ -139,7 +141,7 @@ def test_gpu_semantics_vs_reference_gpu_gallery_image22(rtow, gpu_ctx):
         sums, _ = gpu_ctx.render(cam, p)
         img = device_tonemap(rtow, gpu_ctx, sums, IMAGE22["spp"], rtow.RT_TONEMAP_GPU)
         blk.append(blocks8(img))
-    print("image22", gallery_compare(*blk))
+    print(name, gallery_compare(*blk, name=name))
 
 
 # ------------------------------------------------------------ write_color --
