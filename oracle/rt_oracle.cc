@@ -483,7 +483,7 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
         const float sq = sqrt_k(disc);
         const float q = -(bb + (bb < 0.0f ? -sq : sq));
         if (q != 0.0f) {
-          const float ta = q, tb = cc / q;
+          const float ta = q, tb = cc * (1.0f / q);  // c RN(1/q), the kernel's rcp_k
           const float tr = near ? std::fmin(ta, tb) : std::fmax(ta, tb);
           if (std::isfinite(tr)) t = tr;
         }

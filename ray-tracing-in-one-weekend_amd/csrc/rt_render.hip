@@ -518,7 +518,16 @@ __device__ __forceinline__ void scan_pairs(const RT_CONST pair_geom *__restrict_
 //          r = 1000 ground where |C|^2 - r^2 = 0), whichever has the smaller
 //          intermediate magnitude;
 //   disc = r^2 - |oc - b d|^2 (perpendicular form)  or  b^2 - c;
-//   roots q = -(b + sign(b) sqrt(disc)) and c / q  (no cancellation).
+//   roots q = -(b + sign(b) sqrt(disc)) and c RN(1/q)  (no cancellation).
+// RN(1/q) is rcp_k: v_rcp_f32 and one Newton step, r + r (1 - q r), equal to
+// 1.0f / q for every q whose exponent field is 1..252 (normal q and 1/q),
+// checked exhaustively (tools/ubench_rcp.hip, profiles/r02zj_ubench_rcp.log);
+// here |q| >= sqrt(2^-96).  3 VALU for the second root instead of the ~10 of
+// an IEEE division.
+__device__ __forceinline__ float rcp_k(float q) {
+  const float r = __builtin_amdgcn_rcpf(q);
+  return fmaf(fmaf(-q, r, 1.0f), r, r);
+}
 __device__ __forceinline__ float refine_root(const shade_rec &sr, float t_scan, bool near,
                                              float ox, float oy, float oz, float dx, float dy,
                                              float dz, float o2, float ox2, float oy2, float oz2,
@@ -545,7 +554,7 @@ __device__ __forceinline__ float refine_root(const shade_rec &sr, float t_scan, 
   const float q = -(b + (b < 0.0f ? -sq : sq));
   float t = t_scan;
   if (q != 0.0f) {
-    const float ta = q, tb = c / q;
+    const float ta = q, tb = c * rcp_k(q);
     const float tr = near ? fminf(ta, tb) : fmaxf(ta, tb);
     if (__builtin_isfinite(tr)) t = tr;
   }
