@@ -192,8 +192,12 @@ def main():
     if a.accel == "layer_bvh":
         params.flags |= rtow.RT_FLAG_LAYER_BVH
     tile = torch.zeros((params.local_rows, W, 3), dtype=torch.float32, device=dev)
+    # the step ends like the drop-in CLI's: write_color on the device (src/cpu
+    # arithmetic) turns the tile's sums into bytes, and rank 0 gathers the byte
+    # tiles (3 B per pixel instead of the 12 of the fp32 sums)
+    tile_u8 = torch.zeros((params.local_rows, W, 3), dtype=torch.uint8, device=dev)
     gdev = dev if a.backend == "nccl" else torch.device("cpu")
-    gather_list = ([torch.empty(tile.shape, dtype=tile.dtype, device=gdev) for _ in range(world)]
+    gather_list = ([torch.empty(tile_u8.shape, dtype=tile_u8.dtype, device=gdev) for _ in range(world)]
                    if (world > 1 and rank == 0) else None)
     # a dedicated stream: the kernel, the HIP events timing it and the RCCL gather
     # are all ordered on it (torch's default stream would reach the C ABI as NULL)
@@ -213,8 +217,10 @@ def main():
         ctx.render_async(cam, params, tile.data_ptr(), stream.cuda_stream)
         if events is not None:
             events[1].record(stream)
+        ctx.tonemap_async(tile.data_ptr(), params.local_rows * W, max(spp, 1), tile_u8.data_ptr(),
+                          rtow.RT_TONEMAP_CPU, stream.cuda_stream)
         if world > 1:
-            dist.gather(tile if a.backend == "nccl" else tile.cpu(), gather_list, dst=0)
+            dist.gather(tile_u8 if a.backend == "nccl" else tile_u8.cpu(), gather_list, dst=0)
 
     assert stream.cuda_stream != 0
     first_frame_ms = None
@@ -243,6 +249,8 @@ def main():
         torch.cuda.synchronize(dev)
         barrier()
         elapsed = time.perf_counter() - t0
+    # the last timed frame's sums and bytes (the work frame below reuses the tile)
+    sums_last, u8_last = tile.cpu().numpy(), tile_u8.cpu().numpy()
 
     st = ctx.collect_stats()
     kernel_ms = [e0.elapsed_time(e1) for e0, e1 in evs]
@@ -269,11 +277,12 @@ def main():
         if world > 1:
             tiles = torch.stack(gather_list).cpu().numpy()
         else:
-            tiles = tile.cpu().numpy()[None]
+            tiles = u8_last[None]
         frame = rtow_dist.assemble(tiles, H, world, a.row_block)
-        assert np.isfinite(frame).all() and frame.max() <= spp + 1e-3
+        assert np.isfinite(sums_last).all() and sums_last.max() <= spp + 1e-3
+        assert np.array_equal(u8_last, rtow.tonemap(sums_last, max(spp, 1)))
         if a.out:
-            rtow.write_ppm(a.out, rtow.tonemap(frame, spp), binary=a.out.endswith((".p6", ".pnm")))
+            rtow.write_ppm(a.out, frame, binary=a.out.endswith((".p6", ".pnm")))
 
         k_avg_s = sum(kernel_ms) / len(kernel_ms) / 1e3
         # box_tests counts slab tests (layer BVH) or DDA cell steps (layer grid)
@@ -326,7 +335,7 @@ def main():
             "config": {"workload": workload, "width": W, "height": H, "spp": spp,
                        "max_depth": a.depth, "spheres": scene.n,
                        "parallelism": f"row-interleaved bands of {a.row_block} rows x {world} GPU"
-                                      + ((" + RCCL gather" if a.backend == "nccl" else " + gloo gather")
+                                      + ((" + RCCL gather of byte tiles" if a.backend == "nccl" else " + gloo gather of byte tiles")
                                          if world > 1 else "")},
             "ms_per_frame": round(elapsed / a.steps * 1e3, 3),
             "msamples_per_s": round(samples / elapsed / 1e6, 2),

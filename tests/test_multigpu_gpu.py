@@ -90,14 +90,17 @@ def _bench(args, nproc=1):
     return json.loads(line)
 
 
-def test_bench_two_ranks_gloo_traces_the_same_frames():
+def test_bench_two_ranks_gloo_traces_the_same_frames(tmp_path):
     """bench.py --gpus 2 (gloo rehearsal) renders the same frames as --gpus 1:
-    identical segment totals, both ranks' work counted, gather included."""
+    identical segment totals, both ranks' work counted, and the byte tiles
+    gathered and assembled on rank 0 give the same image, byte for byte."""
     common = ["--steps", "2", "--warmup", "1", "--width", "256", "--height", "144", "--spp", "16",
               "--no-cpu-baseline"]
-    one = _bench(common)
-    two = _bench(common + ["--gpus", "2", "--backend", "gloo"], nproc=2)
+    one = _bench(common + ["--out", str(tmp_path / "one.ppm")])
+    two = _bench(common + ["--gpus", "2", "--backend", "gloo", "--out", str(tmp_path / "two.ppm")], nproc=2)
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
     assert two["segments_per_frame"] == one["segments_per_frame"]
     assert "gloo gather" in two["config"]["parallelism"]
     assert two["value"] > 0 and one["first_frame_ms"] > 0
+    a, b = (tmp_path / "one.ppm").read_bytes(), (tmp_path / "two.ppm").read_bytes()
+    assert a.startswith(b"P3\n256 144\n255\n") and a == b
