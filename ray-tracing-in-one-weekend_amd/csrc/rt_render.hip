@@ -1087,9 +1087,14 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   if (lane == 0) {
     if (STATS) {  // pilot renders (units = 1, launch order): segments per tile
       const kparams k = kernargs();
-      if (k.tile_cost) k.tile_cost[(int)blockIdx.x * kWavesPerBlock + wave] = s;
+      if (k.tile_cost) {
+        // and nothing else: 6 same-address atomics from each of ~10^5 short
+        // waves serialise (the 4-spp pilot took 9.5 ms instead of ~1.2)
+        k.tile_cost[(int)blockIdx.x * kWavesPerBlock + wave] = s;
+        return;
+      }
     }
-    unsigned long long *counters = kernargs().counters;  // (4 atomics per wave)
+    unsigned long long *counters = kernargs().counters;  // (2 atomics per wave, 6 with STATS)
     atomicAdd(&counters[0], (unsigned long long)s);
     atomicAdd(&counters[1], (unsigned long long)steps);
     if (STATS) {
