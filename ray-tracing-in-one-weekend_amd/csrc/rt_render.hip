@@ -70,6 +70,11 @@ constexpr long long kSplitTiles = 12LL * 256 * 4 * 7;
 // tiles) 8.5 / 8.0 / 7.9 / 8.2 ms at 1 / 2 / 3 / 4.
 constexpr long long kPilotTilesPerUnit = 16LL * 256 * 4 * 8;
 constexpr int kUnits = 8;  // without the pilot
+// the per-wave stats counters are spread over 32 slots of 8 (by block index)
+// and summed on the host: ~10^5 waves adding to one address serialise at the
+// end of short launches (1/8 shares: 17.47 vs 17.57 ms slowest rank,
+// profiles/r02zl_ab_counter_slots.log)
+constexpr int kCounterSlots = 32;
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -1094,7 +1099,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         return;
       }
     }
-    unsigned long long *counters = kernargs().counters;  // (2 atomics per wave, 6 with STATS)
+    unsigned long long *counters = kernargs().counters + 8 * (blockIdx.x & (kCounterSlots - 1));
     atomicAdd(&counters[0], (unsigned long long)s);
     atomicAdd(&counters[1], (unsigned long long)steps);
     if (STATS) {
@@ -1847,7 +1852,7 @@ int rt_context_create(int device_ordinal, rt_context **out) {
     if ((e = hipEventCreate(&c->ev0)) != hipSuccess) break;
     if ((e = hipEventCreate(&c->ev1)) != hipSuccess) break;
     if ((e = hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming)) != hipSuccess) break;
-    if ((e = hipMalloc(&c->d_counters, 8 * sizeof(unsigned long long))) != hipSuccess) break;
+    if ((e = hipMalloc(&c->d_counters, 8 * rtk::kCounterSlots * sizeof(unsigned long long))) != hipSuccess) break;
     tonemap_thresholds(c->tonemap_thr64, c->tonemap_thr32);
     if ((e = hipMalloc(&c->d_thr64, sizeof c->tonemap_thr64)) != hipSuccess) break;
     if ((e = hipMalloc(&c->d_thr32, sizeof c->tonemap_thr32)) != hipSuccess) break;
@@ -1996,7 +2001,7 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
   if (prm->flags & RT_FLAG_KEEP_COUNTERS) {
     c->last_samples += samples;
   } else {
-    RT_HIP(hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), st));
+    RT_HIP(hipMemsetAsync(c->d_counters, 0, 8 * rtk::kCounterSlots * sizeof(unsigned long long), st));
     c->last_samples = samples;
   }
   c->last_stats = (prm->flags & RT_FLAG_COUNT_WORK) != 0;
@@ -2165,7 +2170,7 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
 int rt_reset_stats(rt_context *c, void *stream) {
   if (!c) return RT_ERR_INVALID;
   RT_HIP(hipSetDevice(c->device));
-  RT_HIP(hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long),
+  RT_HIP(hipMemsetAsync(c->d_counters, 0, 8 * rtk::kCounterSlots * sizeof(unsigned long long),
                         stream ? (hipStream_t)stream : c->stream));
   c->last_samples = 0;
   return RT_OK;
@@ -2173,9 +2178,10 @@ int rt_reset_stats(rt_context *c, void *stream) {
 
 int rt_collect_stats(rt_context *c, rt_stats *stats) {
   if (!c || !stats) return RT_ERR_INVALID;
-  unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0}, hs[8 * rtk::kCounterSlots];
   RT_HIP(hipSetDevice(c->device));
-  RT_HIP(hipMemcpy(h, c->d_counters, sizeof h, hipMemcpyDeviceToHost));
+  RT_HIP(hipMemcpy(hs, c->d_counters, sizeof hs, hipMemcpyDeviceToHost));
+  for (int i = 0; i < 8 * rtk::kCounterSlots; ++i) h[i & 7] += hs[i];
   stats->segments = h[0];
   stats->wave_steps = h[1];
   stats->samples = c->last_samples;
