@@ -9,10 +9,9 @@ src/gpu's camera model from (-2, 2, 1) towards (0, 0, -1), fp32 write_color
   image20  vfov 90, no defocus   (archive-gpu/image20/camera.h:49-58)
   image21  vfov 20, no defocus   (archive-gpu/image21/camera.h:49-58)
   image22  vfov 20, defocus 10 deg at focus 3.4 (archive-gpu/image22/camera.h:58-71)
-They are the outputs of the reference's CUDA path that can be re-rendered
-here: their scene is fixed (main.cu:24-38), while the final scene's gallery
-image is time-seeded (its archive-gpu/image23 seed-0 scene, restated
-with cuRAND's XORWOW, does not match it either).
+Their scene is fixed (main.cu:24-38).  gallery/gpu/image23.png is src/gpu's
+own final-scene run (1920x1080, 500 spp, main.cu:88 time seed); its seed was
+recovered (tests/gallery_lib.py), so it can be re-rendered here too.
 
 Stored as data, not as the PNG: the exact 8x8 block sums of the 8-bit levels
 per channel (uint16, 135 x 240 x 3; 1080 and 1920 are multiples of 8), which
@@ -28,9 +27,15 @@ from PIL import Image
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CONFIGS = {
-    "image20": "vfov 90, no defocus",
-    "image21": "vfov 20, no defocus",
-    "image22": "vfov 20, defocus 10 deg at focus 3.4",
+    "image20": "five-sphere scene 1920x1080 10spp depth 50, src/gpu camera from (-2, 2, 1) to (0, 0, -1), "
+               "vfov 90, no defocus",
+    "image21": "five-sphere scene 1920x1080 10spp depth 50, src/gpu camera from (-2, 2, 1) to (0, 0, -1), "
+               "vfov 20, no defocus",
+    "image22": "five-sphere scene 1920x1080 10spp depth 50, src/gpu camera from (-2, 2, 1) to (0, 0, -1), "
+               "vfov 20, defocus 10 deg at focus 3.4",
+    # src/gpu's own run: the final scene from time seed 1694284176 (tests/gallery_lib.py)
+    "image23": "src/gpu final scene (seed 1694284176) 1920x1080 500spp depth 50, src/gpu camera from "
+               "(13, 2, 3) to (0, 0, 0), vfov 20, defocus 0.6 at focus 10",
 }
 
 
@@ -42,8 +47,7 @@ def main():
         assert img.shape == (1080, 1920, 3), img.shape
         sums = img.reshape(135, 8, 240, 8, 3).sum(axis=(1, 3)).astype(np.uint16)
         np.savez_compressed(out, blocksum8=sums, source=np.array(f"gallery/gpu/{name}.png"),
-                            config=np.array("five-sphere scene 1920x1080 10spp depth 50, src/gpu camera "
-                                            f"from (-2, 2, 1) to (0, 0, -1), {cam}, fp32 write_color"))
+                            config=np.array(f"{cam}, fp32 write_color"))
         print(out, sums.shape, "mean level", (sums.astype(np.float64) / 64).mean(axis=(0, 1)).round(3))
 
 

@@ -224,3 +224,23 @@ def test_kernel_gpu_semantics_matches_reference_gpu_gallery(rtow, name):
         sums, _ = kernel_render(scene, cam, p, threads=8)
         blk.append(blocks8(rtow.tonemap(sums, IMAGE22["spp"], rtow.RT_TONEMAP_GPU)))
     print(name, gallery_compare(*blk, name=name))
+
+
+def test_src_gpu_scene_of_the_gallery_run(rtow):
+    """tests/gallery_lib.py's restatement of src/gpu's new_world (curand XORWOW,
+    the gallery run's recovered seed): 486 spheres, 373 lambertian / 84 metal /
+    29 dielectric, pinned by a fingerprint of the fp32 arrays (the GPU test
+    against gallery/gpu/image23.png renders exactly this scene)."""
+    from gallery_lib import IMAGE23_SEED, Xorwow, src_gpu_final_scene
+    s = src_gpu_final_scene(rtow)
+    h = hashlib.sha256()
+    for a in (s.cx, s.cy, s.cz, s.radius, s.kind, s.albedo, s.param):
+        h.update(np.ascontiguousarray(a).tobytes())
+    assert IMAGE23_SEED == 1694284176
+    assert s.n == 486 and np.bincount(s.kind).tolist() == [373, 84, 29]
+    assert h.hexdigest()[:16] == "f8b097d4cf72df1a"
+    assert rtow.accel_info(s)["layer_mode"] == 1
+    # curand_uniform lies in (0, 1], so random_float = 1 - it in [0, 1)
+    r = Xorwow(0)
+    u = [r.random_float() for _ in range(10000)]
+    assert min(u) >= 0.0 and max(u) < 1.0
