@@ -152,8 +152,8 @@ def test_final_scene_gpu_semantics_vs_reference_gpu_gallery_image23(rtow, gpu_ct
     Two seeds of ours give the noise floor.  Bounds: image-mean bias <= 0.25
     level per channel (a quarter of north_star's 1/255) and 8x8 block error
     <= 2x our seed-to-seed floor.  Measured: ours is 0.17-0.19 level brighter
-    (the reference's fp32 quadratic traps some grazing rays)
-    and the block error is 1.64x the floor (0.23 vs 0.14 level)."""
+    (0.13-0.14 with the reference's own unrefined fp32 roots) and
+    the block error is 1.64x the floor (0.23 vs 0.14 level)."""
     from gallery_lib import src_gpu_final_scene
     from test_oracle import gallery_blocks
     gpu_ctx.upload(src_gpu_final_scene(rtow))
