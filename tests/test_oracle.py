@@ -192,9 +192,8 @@ def gallery_compare(a, b, name="image22"):
     Bounds: 8x8 block-mean error <= 1.1 x our own seed-to-seed floor, and
     image-mean bias per channel <= max(4 sigma, 0.1 level).  The reference's
     image22 is ~0.05 level darker in red and green than ours (5 sigma at 2 M
-    pixels), most likely the grazing rays its fp32 quadratic traps and the
-    refined roots do not; 0.1 level is a tenth of
-    north_star's 1/255."""
+    pixels), partly from its unrefined fp32 roots (DESIGN.md 4, image23);
+    0.1 level is a tenth of north_star's 1/255."""
     g = gallery_blocks(name)
     n = a.shape[0] * a.shape[1]
     sigma = (a - b).reshape(-1, 3).std(0) / np.sqrt(n)
