@@ -226,7 +226,7 @@ int rt_render_async(rt_context *ctx, const rt_camera *cam, const rt_params *para
 /* Synchronous convenience: render into a context-owned device buffer, time the
  * kernel with hipEvents, copy the sums to HOST memory host_rgb
  * (width*local_rows*3 floats) and fill stats (may be NULL).  kernel_ms spans
- * the render kernel (and the chunk fold), not a first-frame pilot. */
+ * the render kernel (and finish_sums when units > 1), not a first-frame pilot. */
 int rt_render(rt_context *ctx, const rt_camera *cam, const rt_params *params,
               float *host_rgb, rt_stats *stats);
 

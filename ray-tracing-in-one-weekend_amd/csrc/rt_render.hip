@@ -193,7 +193,7 @@ template <class T>
 __device__ __forceinline__ const RT_CONST T *as_const(const T *p) {
   return (const RT_CONST T *)p;
 }
-// per-lane buffers (shading records, frame, chunk sums, counters) in the global
+// per-lane buffers (shading records, frame, counters) in the global
 // address space: global_load/store rather than flat (no lgkmcnt coupling)
 #define RT_GLOBAL __attribute__((address_space(1)))
 template <class T>

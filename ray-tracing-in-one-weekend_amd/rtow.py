@@ -260,8 +260,8 @@ def make_params(width, height, spp, max_depth=50, seed=0, flags=0, rank=0, world
                 units=0):
     """Params for rank `rank` of `world` (interleaved row bands of row_block rows).
 
-    units: waves sharing each tile's sample chunks (0 = automatic); scheduling
-    only, the image is the same for every value (RT_CHUNK_SPP)."""
+    units: waves sharing each tile's samples in even shares (0 = automatic);
+    scheduling only, the image is the same for every value (fixed-point sums)."""
     if world == 1:
         return Params(width, height, spp, max_depth, seed, max(1, height), 1, 0, height, flags, units)
     band_rows = row_block * world
