@@ -821,7 +821,8 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
 // SGPRs, and 6 or 7 waves with more registers ran 2 % slower).  The walk is a serial latency
 // chain per wave (scalar node load -> slab test -> ballot -> branch), so more
 // resident waves keep the VALU busier: 312 vs 322 ms at 7 waves, although the
-// 8-wave budget spills a few per-step values (none inside the walk).  That
+// 8-wave budget spills a few values (none inside the walk; the pool's
+// per-step ones are pinned to VGPRs, see take below).  That
 // became possible once the scene pointers and parameters were re-read from
 // the kernarg segment where they are used (kernargs(), as_const()) instead of
 // being held in SGPRs for the whole kernel: 94 SGPRs + 21 spilled -> 69 at 7
@@ -882,11 +883,16 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   work_ctr wc;  // executed work, STATS builds only
   // take pool item k: slot, sample and pixel; false if the slot is outside the
   // frame (the lane then stays alive without tracing and takes another item)
+  // wave-uniform values the pool reads once per step, held in VGPRs: as SGPRs
+  // they were spilled to VGPR lanes at 8 waves (v_readlane per step)
+  uint32_t s_begin_v = s_begin;
+  uint32_t rowpix_v = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)&s_rowpix[wave][0];
+  asm volatile("" : "+v"(s_begin_v), "+v"(rowpix_v));
   auto take = [&](uint32_t k) -> bool {
     slot = k & 63u;
-    sample = s_begin + (k >> 6);
-    pix = s_rowpix[wave][slot >> 3] + (slot & (kTile - 1));
-    return vmask == ~0ull || ((vmask >> slot) & 1u) != 0;
+    sample = s_begin_v + (k >> 6);
+    pix = ((const __attribute__((address_space(3))) uint32_t *)(uintptr_t)rowpix_v)[slot >> 3] + (slot & (kTile - 1));
+    return ((vmask >> slot) & 1u) != 0;
   };
   // (col, global row) of the lane's pixel: col from the tile origin, row by
   // exact division (pix - col) / W
