@@ -514,6 +514,49 @@ __device__ __forceinline__ void scan_pairs(const RT_CONST pair_geom *__restrict_
   }
 }
 
+// scan_pairs in plain fp32, one sphere at a time: the same fma per sphere as
+// one half of the packed form (the same bits), without splatting the ray terms
+// into VGPR pairs and without moving the second SGPR operand of every
+// v_pk_fma_f32 into a VGPR first (the grid build's extras: 4 spheres a step)
+template <bool OPEN, int NP, bool STATS>
+__device__ __forceinline__ void scan_pairs_scalar(const RT_CONST pair_geom *__restrict__ g, int slot0,
+                                                  const RT_CONST int *__restrict__ orig, const ray_pre &r,
+                                                  hit_state &hs, uint32_t &roots) {
+  float h[2 * NP], e[2 * NP], ks[2 * NP];
+  bool c[2 * NP];
+  uint64_t any = 0;
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    const pair_geom q = cload(g + j);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const float cx = s ? q.cx.y : q.cx.x, cy = s ? q.cy.y : q.cy.x, cz = s ? q.cz.y : q.cz.x;
+      const float hy = fmaf(cy, r.dy.x, r.nk1.x);
+      const float gy = fmaf(cy, r.oy2.x, r.o2.x);
+      const float hh = fmaf(cz, r.dz.x, fmaf(cx, r.dx.x, hy));
+      const float gg = fmaf(cz, r.oz2.x, fmaf(cx, r.ox2.x, gy));
+      const float ee = fmaf(hh, hh, -gg);
+      h[2 * j + s] = hh;
+      e[2 * j + s] = ee;
+      ks[2 * j + s] = s ? q.ks.y : q.ks.x;
+      c[2 * j + s] = ee >= ks[2 * j + s];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2 * NP; ++j) any |= __builtin_amdgcn_ballot_w64(c[j]);
+  if (any) {
+    if (STATS) {
+#pragma unroll
+      for (int j = 0; j < 2 * NP; ++j) roots += __builtin_amdgcn_ballot_w64(c[j]) != 0 ? 1u : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 2 * NP; ++j) {
+      const int i0 = orig ? orig[slot0 + j] : slot0 + j;
+      candidate<OPEN>(c[j], h[j], e[j] - ks[j], tie2_of<OPEN>((uint32_t)i0), hs);
+    }
+  }
+}
+
 // Well-conditioned recomputation of the winning sphere's chosen root.  The
 // scan's expanded quadratic is cheap but, in fp32, near a small sphere's
 // silhouette its root is off by ~1e-4 along the normal: hit points land
@@ -754,8 +797,12 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
     if (p.layer_mode) {
       // the spheres off the layer (in the final scene the ground and the three
       // big spheres) are scanned first: their hits shorten tmax for the walk
-      for (int k = 0; k < p.n_extra_pairs; k += 2)
-        scan_pairs<OPEN, 2, STATS>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, rp, hs, wc.roots);
+      for (int k = 0; k < p.n_extra_pairs; k += 2) {
+        if (GRID)
+          scan_pairs_scalar<OPEN, 2, STATS>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, rp, hs, wc.roots);
+        else
+          scan_pairs<OPEN, 2, STATS>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, rp, hs, wc.roots);
+      }
       if (STATS) wc.tests += 2 * p.n_extra_pairs;
       // every node's y-range lies inside the layer's: its slab interval is
       // computed once per ray, and a node tests x and z only.  Nodes hold

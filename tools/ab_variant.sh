@@ -9,7 +9,7 @@ sed "$expr" ray-tracing-in-one-weekend_amd/csrc/rt_render.hip > $d/src_$name/rt_
 if cmp -s $d/src_$name/rt_render.hip ray-tracing-in-one-weekend_amd/csrc/rt_render.hip; then
   echo "variant $name: sed changed nothing" >&2; exit 1
 fi
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -Iinclude \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -Iinclude \
   -Iray-tracing-in-one-weekend_amd/csrc -shared -o $d/$name.so $d/src_$name/rt_render.hip \
   ray-tracing-in-one-weekend_amd/csrc/rt_host.cpp
 echo "built $d/$name.so"

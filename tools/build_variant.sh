@@ -9,7 +9,7 @@ PKG=$ROOT/ray-tracing-in-one-weekend_amd
 name=$1; src=$2; shift 2
 make -s -C "$PKG" build/obj/rt_sched.o build/obj/rt_host.o
 mkdir -p "$ROOT/build/variants"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I"$ROOT/include" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize -I"$ROOT/include" \
   -I"$PKG/csrc" "$@" -c -o "$ROOT/build/variants/$name.o" "$src"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o "$ROOT/build/variants/$name.so" \
   "$ROOT/build/variants/$name.o" "$PKG/build/obj/rt_sched.o" "$PKG/build/obj/rt_host.o"
