@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 typedef enum {
   RT_OK = 0,
@@ -142,12 +142,19 @@ typedef struct {
 } rt_params;
 
 /* Pixel sums (part of the result, like the RNG): a sample's radiance v (at
- * most 1: albedos must lie in [0, 1]) adds trunc(v * 2^F) to its pixel's
- * uint32 sum, F = 31 - floor(log2(spp)); the frame holds sum * 2^-F.  Integer
- * sums do not depend on the order, so samples can be traced by any lanes,
- * waves (rt_params.units) or GPUs without changing a single bit of the
- * image.  RT_CHUNK_SPP is kept for source compatibility (ABI 2 summed in
- * chunks of 64 samples); nothing depends on it any more. */
+ * most 1: albedos must lie in [0, 1]) adds q(v * 2^F) to its pixel's uint32
+ * sum, F = 31 - floor(log2(spp)); the frame holds sum * 2^-F.  q truncates
+ * for spp < 4096 (F >= 20: a bias below 2^-20 per sample, under 0.03 of a
+ * tonemap level on the darkest visible pixel) and rounds stochastically for
+ * 4096 <= spp < 2^24, trunc(x) + (frac(x) > u) with u a uniform draw keyed by
+ * (pixel, sample): unbiased for every spp the ABI accepts.  Integer sums do
+ * not depend on the order, so samples can be traced by any lanes, waves
+ * (rt_params.units), launches or GPUs without changing a single bit of the
+ * image.  The reference sums in fp64 (src/cpu/main.cc:114-119) or fp32
+ * (src/gpu/camera.h:189-194) with no such format and accepts any albedo;
+ * rt_scene_upload's [0, 1] albedo range is the one deliberate narrowing.
+ * RT_CHUNK_SPP is kept for source compatibility (ABI 1 summed fp32 in chunks
+ * of 64 samples; ABI 2 was never released); nothing depends on it any more. */
 #define RT_CHUNK_SPP 64
 
 typedef struct {
@@ -162,6 +169,7 @@ typedef struct {
   double kernel_ms;      /* hipEvent time of the render kernel (0 if async) */
   uint64_t root_tests;   /* RT_FLAG_COUNT_WORK: per alive lane and bounce, the spheres whose
                             root / interval code the wave executed (some lane's line met it) */
+  uint64_t launches;     /* render kernel launches (bounded sample ranges, RT_OPT_LAUNCH_SAMPLES) */
 } rt_stats;
 
 typedef struct rt_context rt_context;
@@ -203,17 +211,46 @@ int rt_context_create(int device_ordinal, rt_context **out);
 /* Waits for everything enqueued on the context's device, then frees. */
 void rt_context_destroy(rt_context *ctx);
 
+/* Options of a context: placement, shape and launch granularity, never
+ * semantics (every value renders the same image).  value 0 restores the
+ * default; RT_ERR_INVALID for an unknown option or a value out of range.
+ * The structure options are read by the next rt_scene_upload, the launch
+ * option by every render.  They replace environment variables, so a
+ * render's behaviour depends only on its arguments. */
+typedef enum {
+  /* where a launch keeps the layer grid: RT_GRID_AUTO (0),
+   * RT_GRID_LDS (1: cells and items in LDS when they fit), RT_GRID_CELLS_LDS
+   * (2: cells in LDS, items from L1/L2; the cells are built coarser until they
+   * fit), RT_GRID_GLOBAL (3) */
+  RT_OPT_GRID_PLACEMENT = 1,
+  RT_OPT_GRID_SCALE = 2,      /* layer-grid cell side multiplier, 0.05..20 (default 1) */
+  RT_OPT_BVH_LEAF = 3,        /* spheres per BVH leaf, 1..4 (default 4) */
+  RT_OPT_BVH_COLLAPSE = 4,    /* BVH node collapse area ratio (default 0.35) */
+  RT_OPT_BVH_SIDE = 5,        /* SAH weight of the x- and z-facing sides (default 1) */
+  /* at most this many samples (pixels x samples per pixel) per render kernel
+   * launch (default 2^32): a render is split into sample-range launches that
+   * each stay well under a second (no monolithic launch) */
+  RT_OPT_LAUNCH_SAMPLES = 6
+} rt_option;
+enum { RT_GRID_AUTO = 0, RT_GRID_LDS = 1, RT_GRID_CELLS_LDS = 2, RT_GRID_GLOBAL = 3 };
+int rt_context_set_option(rt_context *ctx, int option, double value);
+
 /* Copies the scene to the device (scan records, BVH, shading records) and
  * builds the BVH.  Replaces new_world<<<1,1>>> (src/gpu/main.cu:18-75).
  * Synchronises the device first: renders still running on any stream keep
  * the previous scene.  Centres must be finite, radii finite and non-zero,
  * and the albedos of lambertian and metal spheres in [0, 1] (RT_ERR_INVALID
- * otherwise: the fixed-point pixel sums need a sample's radiance <= 1). */
+ * otherwise: the fixed-point pixel sums need a sample's radiance <= 1 -- a
+ * deliberate narrowing of the reference, which renders energy-creating
+ * albedos too; every scene of the reference is inside it). */
 int rt_scene_upload(rt_context *ctx, const rt_scene_view *scene);
 
 /* Enqueue the render kernel on `stream` (a hipStream_t, NULL = the context's
  * own stream) writing params->width * params->local_rows * 3 floats to the
- * DEVICE pointer accum_rgb.  Replaces render<<<>>> (src/gpu/camera.h:169-195).
+ * DEVICE pointer accum_rgb.  Replaces render<<<>>> (src/gpu/camera.h:169-195),
+ * one monolithic launch in the reference (src/gpu/main.cu:130): here the
+ * samples are split into launches of at most RT_OPT_LAUNCH_SAMPLES samples,
+ * each checked for a launch error as it is enqueued.
  * Does not synchronise, also not on the first render of a frame geometry
  * with RT_FLAG_PILOT_SCHEDULE (the pilot and its sort are enqueued too).
  * Renders of one context on different streams run one after another (each
@@ -226,7 +263,9 @@ int rt_render_async(rt_context *ctx, const rt_camera *cam, const rt_params *para
 /* Synchronous convenience: render into a context-owned device buffer, time the
  * kernel with hipEvents, copy the sums to HOST memory host_rgb
  * (width*local_rows*3 floats) and fill stats (may be NULL).  kernel_ms spans
- * the render kernel (and finish_sums when units > 1), not a first-frame pilot. */
+ * the render launches (and finish_sums when several units or launches share a
+ * tile), not a first-frame pilot.  Waits launch by launch, so a device fault
+ * is reported after the launch it happened in. */
 int rt_render(rt_context *ctx, const rt_camera *cam, const rt_params *params,
               float *host_rgb, rt_stats *stats);
 
@@ -272,7 +311,7 @@ int rt_write_ppm(int fd, const uint8_t *rgb, int width, int height, int binary);
 
 /* Known-answer evaluation of the render kernel's own device arithmetic on
  * `device` (synchronous).  10 doubles in, 9 out per case (layouts in
- * rt_render.hip, kat_kernel):
+ * rt_kernel.hip, kat_kernel):
  *   RT_KAT_SPHERE_HIT   sphere::hit            src/cpu/sphere.h:24-51
  *   RT_KAT_REFLECT      reflect                src/cpu/vec3.h:122-124
  *   RT_KAT_REFRACT      refract                src/cpu/vec3.h:126-131
@@ -280,11 +319,20 @@ int rt_write_ppm(int fd, const uint8_t *rgb, int width, int height, int binary);
 enum { RT_KAT_SPHERE_HIT = 0, RT_KAT_REFLECT = 1, RT_KAT_REFRACT = 2, RT_KAT_REFLECTANCE = 3 };
 int rt_device_kat(int device, int kind, const double *in, size_t n_cases, double *out);
 
-/* Host only (no device): what rt_scene_upload would build for `scene` --
+/* Host only (no device): what rt_scene_upload would build for `scene` with
+ * the given RT_OPT_GRID_PLACEMENT / RT_OPT_GRID_SCALE values (0 = default) --
  * BVH size, layer split, layer-grid dimensions, LDS footprint and the grid's
  * invariants (cell i's items are [first_i, first_{i+1}); ring cells empty).
- * out[16], layout in rt_render.hip.  For tests and sanitizer runs. */
-int rt_internal_accel_info(const rt_scene_view *scene, uint64_t *out);
+ * Writes min(n_out, RT_ACCEL_INFO_N) values:
+ *   0 nodes per DFS order   1 BVH slots          2 layer mode     3 extra_pair0
+ *   4 n_extra_pairs         5 grid_nx (w/ ring)  6 grid_nz        7 grid items
+ *   8 grid LDS bytes        9 whole grid in LDS 10 max items/cell 11 start invariant
+ *  12 empty ring cells ok  13 oref * 1000      14 layer slots    15 listed cells
+ *  16 placement (RT_GRID_*, 0: no grid)         17 cell scale * 1000
+ * For tests and sanitizer runs. */
+#define RT_ACCEL_INFO_N 18
+int rt_internal_accel_info(const rt_scene_view *scene, int grid_placement, double grid_scale, uint64_t *out,
+                           size_t n_out);
 
 #ifdef __cplusplus
 }

@@ -364,7 +364,16 @@ struct kctx {
   const rt_params *p;
   uint32_t seed32;
   bool open, metal_unit;
+  double *exact = nullptr;  // rto_kernel_render_exact: fp64 sums of the unquantised radiance
+  const float *out0 = nullptr;  // ... indexed like the frame tile out0
+  bool no_dither = false;   // ... and the format without stochastic rounding (truncation only)
 };
+
+// the sum format's dither draw (rt_kernel.hip dither_u): pcg4d keyed by the
+// pixel and the sample with the bit-inverted seed
+inline float dither_u(uint32_t pix, uint32_t sample, uint32_t seed32) {
+  return unif(pcg4d(pix, sample, 0u, ~seed32).x);
+}
 
 void camera_ray(const kctx &k, uint32_t pix, int col, int grow, uint32_t sample, float o[3],
                 float d[3]) {
@@ -402,14 +411,18 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
   const size_t n = sc.cx.size();
   unsigned long long segs = 0;
   // fixed-point pixel sum (the kernel's spec): a sample's
-  // radiance v (at most 1) adds trunc(v 2^F) to a uint32 sum, F = 31 -
-  // floor(log2(spp)); the pixel is sum 2^-F.  Integer addition does not depend
-  // on the order, so any lanes, waves or GPUs may trace a pixel's samples
+  // radiance v (at most 1) adds q(v 2^F) to a uint32 sum, F = 31 -
+  // floor(log2(spp)); the pixel is sum 2^-F.  q truncates for F >= 20 and
+  // rounds stochastically below, trunc(x) + (frac(x) > u).  Integer addition
+  // does not depend on the order, so any lanes, waves, launches or GPUs may
+  // trace a pixel's samples
   acc[0] = acc[1] = acc[2] = 0.0f;
+  double ex[3] = {0.0, 0.0, 0.0};
   if (k.p->max_depth <= 0 || k.p->spp <= 0) return 0;  // ray_color(.., 0) is black, no hit test
   int f = 31;
   for (int s = k.p->spp; s > 1; s >>= 1) --f;
   const float qscale = std::ldexp(1.0f, f), qinv = std::ldexp(1.0f, -f);
+  const bool dither = f < 20 && !k.no_dither;
   uint32_t q[3] = {0u, 0u, 0u};
   for (uint32_t sample = 0; sample < (uint32_t)k.p->spp; ++sample) {
     float o[3], d[3];
@@ -432,16 +445,30 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
         tmax = INFINITY;
         best = -1;
         near = true;
-        for (size_t i = 0; i < n; ++i) {
-          const float h = fmaf_(sc.cz[i], d[2], fmaf_(sc.cx[i], d[0], fmaf_(sc.cy[i], d[1], nk1)));
-          const float g = fmaf_(sc.cz[i], oz2, fmaf_(sc.cx[i], ox2, fmaf_(sc.cy[i], oy2, o2)));
-          const float e = fmaf_(h, h, -g);
-          if (e >= sc.ks[i]) {
+        // the per-sphere test in blocks of 64: a branch-free pass the compiler
+        // vectorises (h and the discriminant's excess for every sphere), then
+        // the candidates in index order -- the same arithmetic per sphere
+        constexpr size_t kB = 64;
+        float hb[kB], eb[kB];
+        for (size_t i0 = 0; i0 < n; i0 += kB) {
+          const size_t m = std::min(kB, n - i0);
+          const float *cx = &sc.cx[i0], *cy = &sc.cy[i0], *cz = &sc.cz[i0], *ks = &sc.ks[i0];
+          for (size_t j = 0; j < m; ++j) {
+            const float h = fmaf_(cz[j], d[2], fmaf_(cx[j], d[0], fmaf_(cy[j], d[1], nk1)));
+            const float g = fmaf_(cz[j], oz2, fmaf_(cx[j], ox2, fmaf_(cy[j], oy2, o2)));
+            hb[j] = h;
+            eb[j] = fmaf_(h, h, -g) - ks[j];  // >= 0 <=> e >= ks (exact for finite floats)
+          }
+          for (size_t j = 0; j < m; ++j) {
+          if (!(eb[j] >= 0.0f)) continue;
+          const size_t i = i0 + j;
+          const float h = hb[j];
+          {
             // sphere.h:34-44: the root offered is t0 if past t_min, else t1; it
             // wins if closer than tmax (ties: last index for the closed src/cpu
             // interval, first for the open src/gpu one -- what a sequential scan
             // does, stated so that any visiting order gives the same winner)
-            const float sq = sqrt_k(e - sc.ks[i]);
+            const float sq = sqrt_k(eb[j]);
             const float t0 = h - sq, t1 = h + sq;
             const bool use0 = k.open ? t0 > 0.001f : t0 >= 0.001f;
             const float root = use0 ? t0 : t1;
@@ -449,12 +476,13 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
             const bool closer = root < tmax || (root == tmax && (k.open ? (long)i < best : (long)i > best));
             if (tr)
               std::fprintf(g_trace, "   cand %zu disc=%.9g t0=%.9g t1=%.9g root=%.9g above=%d closer=%d\n", i,
-                           e - sc.ks[i], t0, t1, root, (int)above, (int)closer);
+                           eb[j], t0, t1, root, (int)above, (int)closer);
             if (above && closer) {
               tmax = root;
               near = use0;
               best = (long)i;
             }
+          }
           }
         }
       };
@@ -514,7 +542,12 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
         const float a = 0.5f * (d[1] + 1.0f);
         const float s0 = 1.0f - a;
         const float v[3] = {th[0] * fmaf_(a, 0.5f, s0), th[1] * fmaf_(a, 0.7f, s0), th[2] * (s0 + a)};
-        for (int j = 0; j < 3; ++j) q[j] += (uint32_t)(v[j] * qscale);
+        const float u = dither ? dither_u(pix, sample, k.seed32) : 0.0f;
+        for (int j = 0; j < 3; ++j) {
+          const float x = v[j] * qscale;
+          q[j] += (uint32_t)x + (dither && x - std::floor(x) > u ? 1u : 0u);
+          ex[j] += (double)v[j];
+        }
         break;
       }
       const size_t b = (size_t)best;
@@ -572,6 +605,10 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
           for (int a = 0; a < 3; ++a) sd[a] = fmaf_(m, nn[a], q[a]);
         }
       }
+      // an opaque sphere hit from inside ends the path:
+      // inside a lambertian or metal sphere every scatter points inward, so
+      // the reference's path would stay inside to the depth cap (black)
+      scattered = scattered && (front || sc.kind[b] == RT_DIELECTRIC);
       ++depth;
       if (!scattered || depth >= k.p->max_depth) break;
       for (int a = 0; a < 3; ++a) {
@@ -582,6 +619,10 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
     }
   }
   for (int a = 0; a < 3; ++a) acc[a] = (float)q[a] * qinv;
+  if (k.exact) {
+    double *e = k.exact + 3 * ((size_t)(&acc[0] - k.out0) / 3);
+    for (int a = 0; a < 3; ++a) e[a] = ex[a];
+  }
   return segs;
 }
 
@@ -668,14 +709,19 @@ int rto_reference_render(int width, double aspect, int spp, int max_depth, int s
   return 0;
 }
 
-int rto_kernel_render(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
-                      float *out, unsigned long long *segments, int threads) {
+int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
+                            float *out, double *exact, int no_dither, unsigned long long *segments,
+                            int threads) {
   if (!scene || !cam || !p || !out || p->width < 1 || p->height < 1 || p->row_block < 1 ||
-      p->band_stride < 1 || p->local_rows < 0)
+      p->band_stride < 1 || p->local_rows < 0 || p->spp < 0 || p->spp >= (1 << 24))
     return -1;
   const kscene sc = make_kscene(*scene);
   kctx k{&sc, cam, p, (uint32_t)p->seed ^ ((uint32_t)(p->seed >> 32) * 0x9E3779B9u),
          (p->flags & RT_FLAG_OPEN_INTERVAL) != 0, (p->flags & RT_FLAG_METAL_UNIT_VECTOR) != 0};
+  k.exact = exact;
+  k.out0 = out;
+  k.no_dither = no_dither != 0;
+  if (exact) std::memset(exact, 0, 3 * sizeof(double) * (size_t)p->local_rows * (size_t)p->width);
   if (threads < 1) {
     // the machine's cores, but no more than OMP_NUM_THREADS (16 on the GPU
     // box, whose nproc shows the whole host) or 16
@@ -709,6 +755,11 @@ int rto_kernel_render(const rt_scene_view *scene, const rt_camera *cam, const rt
   for (auto &t : pool) t.join();
   if (segments) *segments = total.load();
   return 0;
+}
+
+int rto_kernel_render(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
+                      float *out, unsigned long long *segments, int threads) {
+  return rto_kernel_render_exact(scene, cam, p, out, nullptr, 0, segments, threads);
 }
 
 int rto_trace(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p, int col,

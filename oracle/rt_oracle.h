@@ -17,6 +17,14 @@ int rto_reference_render(int width, double aspect, int spp, int max_depth, int s
 /* fp32 restatement of the kernel algorithm; same arguments as rt_render. */
 int rto_kernel_render(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
                       float *out, unsigned long long *segments, int threads);
+/* The same, plus (exact != NULL) each pixel's fp64 sum of the unquantised
+ * sample radiances (3 doubles per pixel, laid out like out) -- the reference's
+ * own accumulation (src/cpu/main.cc:114-119) of the same samples -- and, with
+ * no_dither, the sum format without its stochastic rounding (truncation at
+ * every spp: the round-2 format, for the test that shows why it changed). */
+int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
+                            float *out, double *exact, int no_dither, unsigned long long *segments,
+                            int threads);
 /* fp64 final scene rows: kind, cx, cy, cz, r, albedo rgb, param (9 doubles). */
 /* debug: print one sample's segments and candidates to stdout */
 int rto_trace(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p, int col,

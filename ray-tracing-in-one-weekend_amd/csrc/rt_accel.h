@@ -1,0 +1,54 @@
+// rt_accel.h -- internal to librtow: the host-side builder of the render
+// kernel's scene records and acceleration structures (rt_accel.cpp), used by
+// rt_scene_upload and rt_internal_accel_info (rt_api.cpp).
+#ifndef RTOW_RT_ACCEL_H
+#define RTOW_RT_ACCEL_H
+
+#include <cstdint>
+#include <vector>
+
+#include "rt.h"
+#include "rt_layout.h"
+
+namespace rtk {
+
+// builder options (rt_context_set_option; scheduling and placement only:
+// every value renders the same image)
+struct accel_options {
+  int bvh_leaf = 4;          // RT_OPT_BVH_LEAF: spheres per BVH leaf, 1..4
+  double collapse = 0.35;    // RT_OPT_BVH_COLLAPSE
+  double side = 1.0;         // RT_OPT_BVH_SIDE
+  double grid_scale = 1.0;   // RT_OPT_GRID_SCALE
+  int grid_placement = -1;   // RT_OPT_GRID_PLACEMENT: -1 auto, else kGridGlobal / kGridLds / kGridCells
+};
+
+// everything rt_scene_upload copies to the device, plus the builder's facts
+struct accel_build {
+  uint32_t n = 0, n_pad = 0;
+  std::vector<pair_geom> scan_geom;  // brute-force order, n_pad / 2 pairs
+  std::vector<shade_rec> shade;      // n
+  std::vector<pair_geom> bvh_geom;   // BVH leaf order (+ extras in layer mode)
+  std::vector<int> slots;            // BVH slot -> original index, -1 padding
+  std::vector<bvh_node> nodes;       // 8 DFS orders
+  size_t per_order = 0;
+  double oref = 64.0;
+  bool layer_mode = false;
+  float layer_lo = 0.0f, layer_hi = 0.0f, layer_cy = 0.0f;
+  uint32_t extra_pair0 = 0, n_extra_pairs = 0;
+  // layer grid (empty: none)
+  std::vector<uint32_t> grid_cells;
+  std::vector<float> grid_items;  // 4 floats per item
+  float grid_x0 = 0, grid_z0 = 0, grid_xi = 0, grid_zi = 0, grid_x1 = 0, grid_z1 = 0, grid_g = 0;
+  int grid_nx = 0, grid_nz = 0;
+  double grid_scale = 1.0;        // the cell scale the grid was built with
+  int grid_placement = kGridGlobal;
+};
+
+// arrays present, known materials, finite centres and radii, non-zero radii,
+// albedos in [0, 1] (rt_scene_upload's contract, include/rt.h)
+bool scene_ok(const rt_scene_view *s);
+void build_accel(const rt_scene_view *s, const accel_options &o, accel_build &out);
+
+}  // namespace rtk
+
+#endif  // RTOW_RT_ACCEL_H

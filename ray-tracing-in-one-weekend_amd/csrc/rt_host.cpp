@@ -1,6 +1,6 @@
 // rt_host.cpp -- host-side pieces of the render path that run once per frame:
 // scene construction, camera setup, tonemap and PPM output.  Pure C++17, no
-// HIP calls (the device half lives in rt_render.hip).
+// HIP calls (the device half lives in rt_kernel.hip and rt_api.cpp).
 //
 // Scene construction restates random_scene() (src/cpu/main.cc:32-76) with the
 // std::mt19937 draws SEQUENCED EXPLICITLY in the order g++ 11 evaluates the

@@ -9,7 +9,7 @@
 // block order -- what std::stable_sort did on the host in round 1) and the
 // expansion by units.  Temporaries are stream-ordered allocations, so
 // rt_render_async stays asynchronous on the first render of a geometry too.
-// Kept apart from rt_render.hip so that the hipcub instantiations do not slow
+// Kept apart from rt_kernel.hip so that the hipcub instantiations do not slow
 // down rebuilding the render kernel.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -18,7 +18,7 @@
 
 namespace {
 
-constexpr int kWavesPerBlock = 4;  // = rtk::kWavesPerBlock (rt_render.hip)
+constexpr int kWavesPerBlock = 4;  // = rtk::kWavesPerBlock (rt_layout.h)
 
 __global__ __launch_bounds__(256) void block_costs(const uint32_t *__restrict__ tile_cost, uint32_t blocks,
                                                    uint32_t *__restrict__ cost, uint32_t *__restrict__ idx) {

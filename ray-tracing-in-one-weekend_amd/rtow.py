@@ -37,7 +37,12 @@ RT_FLAG_LAYER_BVH = 1 << 12  # layer scenes: walk the layer BVH instead of the l
 RT_CHUNK_SPP = 64  # include/rt.h: kept for compatibility (pixel sums are exact integers, units split evenly)
 RT_TONEMAP_CPU, RT_TONEMAP_GPU = 0, 1  # write_color of src/cpu (fp64) / src/gpu (fp32)
 RT_KAT_SPHERE_HIT, RT_KAT_REFLECT, RT_KAT_REFRACT, RT_KAT_REFLECTANCE = 0, 1, 2, 3
-ABI_VERSION = 3
+ABI_VERSION = 4
+# rt_context_set_option (include/rt.h): placement / shape / launch options, never semantics
+RT_OPT_GRID_PLACEMENT, RT_OPT_GRID_SCALE, RT_OPT_BVH_LEAF = 1, 2, 3
+RT_OPT_BVH_COLLAPSE, RT_OPT_BVH_SIDE, RT_OPT_LAUNCH_SAMPLES = 4, 5, 6
+RT_GRID_AUTO, RT_GRID_LDS, RT_GRID_CELLS_LDS, RT_GRID_GLOBAL = 0, 1, 2, 3
+GRID_PLACEMENTS = {"auto": RT_GRID_AUTO, "lds": RT_GRID_LDS, "cells": RT_GRID_CELLS_LDS, "global": RT_GRID_GLOBAL}
 
 _f = ctypes.POINTER(ctypes.c_float)
 _u32 = ctypes.POINTER(ctypes.c_uint32)
@@ -75,7 +80,8 @@ class Stats(ctypes.Structure):
                 ("bf_tests", ctypes.c_uint64), ("sphere_tests", ctypes.c_uint64),
                 ("box_tests", ctypes.c_uint64), ("box_hits", ctypes.c_uint64),
                 ("wave_steps", ctypes.c_uint64),
-                ("kernel_ms", ctypes.c_double), ("root_tests", ctypes.c_uint64)]
+                ("kernel_ms", ctypes.c_double), ("root_tests", ctypes.c_uint64),
+                ("launches", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -131,7 +137,9 @@ def lib():
                                     ctypes.c_void_p]
         L.rt_write_ppm.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                    ctypes.c_int]
-        L.rt_internal_accel_info.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.rt_internal_accel_info.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double,
+                                             ctypes.c_void_p, ctypes.c_size_t]
+        L.rt_context_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
         _lib = L
     return _lib
 
@@ -309,7 +317,17 @@ class Context:
         except Exception:
             pass
 
-    def upload(self, scene):
+    def set_option(self, option, value):
+        """rt_context_set_option: placement / shape / launch granularity (0 = default)."""
+        check(lib().rt_context_set_option(self._h, option, float(value)), "rt_context_set_option")
+
+    def upload(self, scene, grid_mode=None, grid_scale=None):
+        """rt_scene_upload; grid_mode ("auto", "lds", "cells", "global") and
+        grid_scale set the layer grid's options first (the image is the same)."""
+        if grid_mode is not None:
+            self.set_option(RT_OPT_GRID_PLACEMENT, GRID_PLACEMENTS[grid_mode])
+        if grid_scale is not None:
+            self.set_option(RT_OPT_GRID_SCALE, grid_scale)
         v = scene.view()
         check(lib().rt_scene_upload(self._h, ctypes.byref(v)), "rt_scene_upload")
         self.scene = scene
@@ -366,15 +384,17 @@ def device_kat(kind, cases, device=0):
 ACCEL_INFO_KEYS = ("nodes_per_order", "bvh_slots", "layer_mode", "extra_pair0", "n_extra_pairs",
                    "grid_nx", "grid_nz", "grid_items", "grid_lds_bytes", "grid_fits_lds",
                    "max_items_per_cell", "grid_starts_ok", "grid_ring_empty", "oref_milli",
-                   "layer_slots", "listed_cells")
+                   "layer_slots", "listed_cells", "grid_placement", "grid_scale_milli")
 
 
-def accel_info(scene):
-    """What rt_scene_upload would build for `scene`, computed on the host
-    (rt_internal_accel_info; no device): a dict of ACCEL_INFO_KEYS."""
+def accel_info(scene, grid_mode="auto", grid_scale=0.0):
+    """What rt_scene_upload would build for `scene` with those grid options,
+    computed on the host (rt_internal_accel_info; no device): a dict of
+    ACCEL_INFO_KEYS."""
     v = scene.view()
-    out = np.zeros(16, np.uint64)
-    check(lib().rt_internal_accel_info(ctypes.byref(v), out.ctypes.data), "rt_internal_accel_info")
+    out = np.zeros(len(ACCEL_INFO_KEYS), np.uint64)
+    check(lib().rt_internal_accel_info(ctypes.byref(v), GRID_PLACEMENTS[grid_mode], float(grid_scale),
+                                       out.ctypes.data, out.size), "rt_internal_accel_info")
     return {k: int(x) for k, x in zip(ACCEL_INFO_KEYS, out)}
 
 

@@ -21,6 +21,10 @@ def lib():
     if _lib is None:
         if not os.path.exists(ORACLE_SO):
             raise RuntimeError(f"{ORACLE_SO} missing: run `make -C oracle`")
+        # built with -mfma (oracle/Makefile): the host CPU needs FMA3
+        with open("/proc/cpuinfo") as f:
+            if " fma " not in f.read().replace("\n", " "):
+                raise RuntimeError("the oracle is built with -mfma but this CPU has no FMA3")
         L = ctypes.CDLL(ORACLE_SO)
         L.rto_reference_render.argtypes = [ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
@@ -55,6 +59,24 @@ def kernel_render(scene, cam, params, threads=0):
     assert lib().rto_kernel_render(ctypes.addressof(v), ctypes.addressof(cam), ctypes.addressof(params),
                                    out.ctypes.data, ctypes.byref(seg), threads) == 0
     return out, seg.value
+
+
+def kernel_render_exact(scene, cam, params, no_dither=False, threads=0):
+    """kernel_render plus each pixel's fp64 sum of the unquantised sample
+    radiances (the reference's fp64 accumulation, src/cpu/main.cc:114-119, of
+    the same samples) -> (float32 sums, float64 exact sums, segments).
+    no_dither: the sum format without stochastic rounding (truncation)."""
+    v = scene.view()
+    out = np.zeros((params.local_rows, params.width, 3), np.float32)
+    exact = np.zeros((params.local_rows, params.width, 3), np.float64)
+    seg = ctypes.c_ulonglong()
+    L = lib()
+    L.rto_kernel_render_exact.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int, ctypes.POINTER(ctypes.c_ulonglong),
+                                                                   ctypes.c_int]
+    assert L.rto_kernel_render_exact(ctypes.addressof(v), ctypes.addressof(cam), ctypes.addressof(params),
+                                     out.ctypes.data, exact.ctypes.data, int(no_dither), ctypes.byref(seg),
+                                     threads) == 0
+    return out, exact, seg.value
 
 
 def trace(scene, cam, params, col, row, sample, max_depth=50):

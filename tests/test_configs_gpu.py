@@ -203,16 +203,15 @@ def test_pilot_first_render_is_asynchronous_and_correct(rtow):
             assert np.array_equal(t.cpu().numpy(), want), (w, h)
 
 
-def test_lds_resident_grid_equals_global_grid(rtow, gpu_ctx, monkeypatch):
-    """The layer grid copied into LDS (render_kernel GLDS build, the default
-    when it fits 17 KB) and the same grid read from global memory
-    (RTOW_GRID_LDS=0 at upload) give the same bits, with split chunks and the
-    pilot schedule too."""
+def test_lds_resident_grid_equals_global_grid(rtow, gpu_ctx):
+    """The layer grid copied into LDS (render_kernel placement kGridLds, the
+    default when it fits 17 KB), its cells alone in LDS (kGridCells) and the
+    grid read from global memory (RT_OPT_GRID_PLACEMENT) give the same bits,
+    with split units and the pilot schedule too."""
     cam = rtow.camera_cpu(aspect=640 / 360)
     outs = []
-    for lds in ("0", "1"):
-        monkeypatch.setenv("RTOW_GRID_LDS", lds)
-        gpu_ctx.upload(rtow.final_scene())
+    for mode in ("global", "lds", "cells"):
+        gpu_ctx.upload(rtow.final_scene(), grid_mode=mode)
         for flags, units in ((GRID, 1), (GRID | rtow.RT_FLAG_PILOT_SCHEDULE, 3)):
             outs.append(gpu_ctx.render(cam, rtow.make_params(640, 360, 130, seed=21, flags=flags, units=units)))
     ref, sref = outs[0]
@@ -248,3 +247,108 @@ def test_scene_upload_rejects_albedo_outside_unit_interval(rtow):
         ctx.upload(dataclasses.replace(base, albedo=alb))
         same, _ = ctx.render(cam, prm)
         assert np.array_equal(before, same)
+
+
+# ---- round 3: the configs at their own sample counts, the sum format's
+# ---- headroom, its stochastic rounding, bounded launches, grid placements
+
+@pytest.mark.parametrize("units", [1, 0])
+def test_c3_band_at_1000spp_bit_exact_vs_oracle(rtow, gpu_ctx, oracle, units):
+    """C3 at its own 1000 spp (F = 22: a sample adds up to 2^22, 1000 of them
+    up to 4.19e9 of the uint32's 4.29e9): one full-width 8-row band of the
+    7680x4320 frame (rank 0 of the 540-way band split), one wave per tile and
+    the automatic split (8 units: the band has 960 tiles), bit-exact vs the
+    oracle with equal segments (/root/reference/src/cpu/main.cc:111-123)."""
+    scene = rtow.final_scene()
+    gpu_ctx.upload(scene)
+    cam = rtow.camera_cpu(aspect=7680 / 4320)
+    p = band_params(rtow, 7680, 4320, 1000, 540, 0, seed=310, flags=GRID, units=units)
+    assert p.local_rows == 8
+    got, st = gpu_ctx.render(cam, p)
+    want, segs = kernel_render(scene, cam, p)
+    assert np.array_equal(got, want), int((got != want).sum())
+    assert st.segments == segs and st.samples == 7680 * 8 * 1000
+
+
+@pytest.mark.parametrize("mode,units", [("cells", 1), ("cells", 0), ("global", 0)])
+def test_c4_scene_at_2000spp_bit_exact_vs_oracle(rtow, gpu_ctx, oracle, mode, units):
+    """C4's scene (10 000 spheres), camera (aspect 1) and own 2000 spp (F =
+    21), rank 0's first 8-row band of a 64x64 frame split 8 ways (the
+    oracle's brute force over 10 004 spheres sizes the frame), with the grid's
+    cells in LDS (the automatic placement for this scene) and in global
+    memory, one unit and the automatic split: bit-exact vs the oracle."""
+    scene = rtow.final_scene(half_extent=50)
+    gpu_ctx.upload(scene, grid_mode=mode)
+    assert rtow.accel_info(scene, mode)["grid_placement"] == (rtow.RT_GRID_CELLS_LDS if mode == "cells"
+                                                              else rtow.RT_GRID_GLOBAL)
+    cam = rtow.camera_cpu(aspect=1.0)
+    p = band_params(rtow, 64, 64, 2000, 8, 0, rows=8, seed=410, flags=GRID, units=units)
+    got, st = gpu_ctx.render(cam, p)
+    want, segs = kernel_render(scene, cam, p)
+    assert np.array_equal(got, want), int((got != want).sum())
+    assert st.segments == segs
+
+
+@pytest.mark.parametrize("spp", [1000, 2000, 2047, 4096])
+def test_all_sky_frame_uses_the_sum_headroom_without_wrapping(rtow, gpu_ctx, oracle, spp):
+    """A 64x64 frame of sky only (camera looking straight up): under src/cpu
+    semantics a sky sample's blue radiance is exactly 1 (s0 + a with s0 = 1 -
+    a), so every pixel's blue sum is spp * 2^F -- 4.19e9 at 1000 spp, 4.19e9
+    at 2000, 4.29e9 at 2047, within 2^F of the uint32 limit -- and must come
+    out as exactly spp, with no wrap; red and green equal the oracle's bits.
+    4096 spp runs the stochastic rounding (F = 19)."""
+    scene = rtow.final_scene()
+    gpu_ctx.upload(scene)
+    cam = rtow.camera_cpu(lookfrom=(30, 5, 30), lookat=(30, 100, 30.001), vup=(0, 0, 1), vfov=20.0, aspect=1.0,
+                          aperture=0.0)
+    p = rtow.make_params(64, 64, spp, seed=5, flags=GRID)
+    got, st = gpu_ctx.render(cam, p)
+    assert st.segments == 64 * 64 * spp  # one segment per sample: all sky
+    assert np.all(got[..., 2] == np.float32(spp))
+    assert np.all(got[..., :2] <= spp) and np.all(got[..., :2] > 0.5 * spp)
+    want, segs = kernel_render(scene, cam, p)
+    assert np.array_equal(got, want), int((got != want).sum())
+
+
+def test_stochastic_rounding_bit_exact_vs_oracle(rtow, gpu_ctx, oracle):
+    """spp >= 4096 switches the sums to stochastic rounding (F < 20): the
+    kernel's dither draw and rounding equal the oracle's bit for bit, on the
+    final scene at 4096 spp, with units 1 and 5 and two bounded launches."""
+    scene = rtow.final_scene()
+    gpu_ctx.upload(scene)
+    cam = rtow.camera_cpu(aspect=32 / 18)
+    p = rtow.make_params(32, 18, 4096, seed=44, flags=GRID, units=1)
+    want, segs = kernel_render(scene, cam, p)
+    for units, budget in ((1, 0), (5, 0), (1, 32 * 18 * 2048)):
+        gpu_ctx.set_option(rtow.RT_OPT_LAUNCH_SAMPLES, budget)
+        p.units = units
+        got, st = gpu_ctx.render(cam, p)
+        assert np.array_equal(got, want), (units, budget, int((got != want).sum()))
+        assert st.segments == segs and st.launches == (2 if budget else 1)
+    gpu_ctx.set_option(rtow.RT_OPT_LAUNCH_SAMPLES, 0)
+
+
+def test_bounded_launches_give_the_same_image(rtow, gpu_ctx):
+    """a render is split into sample-range launches of at most
+    RT_OPT_LAUNCH_SAMPLES samples.  C4's rank-0 share (2048 x 16384 pixels,
+    10 000 spheres) at 16 spp with a budget of 2^26 samples runs as 8
+    launches; its image and segments equal the one-launch render bit for bit,
+    and so do 3 launches with 2 units per tile.  At the default budget
+    (2^32) the headline frame (3840x2160x500 = 4.15e9 samples) stays one
+    launch, and C4's full share at 2000 spp (6.7e10) would be 16."""
+    scene = rtow.final_scene(half_extent=50)
+    gpu_ctx.upload(scene)
+    cam = rtow.camera_cpu(aspect=1.0)
+    p = band_params(rtow, 16384, 16384, 16, 8, 0, seed=420, flags=GRID, units=1)
+    one, s1 = gpu_ctx.render(cam, p)
+    assert s1.launches == 1
+    for budget, units, launches in ((1 << 26, 1, 8), (2048 * 16384 * 6, 2, 3)):
+        gpu_ctx.set_option(rtow.RT_OPT_LAUNCH_SAMPLES, budget)
+        p.units = units
+        img, st = gpu_ctx.render(cam, p)
+        assert st.launches == launches
+        same(one, s1, img, st)
+        assert st.kernel_ms / st.launches < 1000.0
+    gpu_ctx.set_option(rtow.RT_OPT_LAUNCH_SAMPLES, 0)
+    with pytest.raises(rtow.RTError):
+        gpu_ctx.set_option(rtow.RT_OPT_LAUNCH_SAMPLES, -5)

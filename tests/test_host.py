@@ -167,7 +167,7 @@ def test_ppm_writer_p3_and_p6(rtow, tmp_path):
 def test_abi_exports_every_declared_symbol(rtow):
     hdr = open(os.path.join(ROOT, "include", "rt.h")).read()
     names = sorted(set(re.findall(r"^\s*(?:[\w\*\s]+?)\b(rt_\w+)\s*\(", hdr, re.M)))
-    assert len(names) == 21, names
+    assert len(names) == 22, names
     L = rtow.lib()
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
@@ -182,7 +182,7 @@ def test_invalid_arguments_return_status(rtow):
     assert L.rt_scene_final(11, None, None) == -1
     assert L.rt_tonemap_u8(None, 4, 10, None) == -1
     assert L.rt_strerror(-4) == b"no such HIP device"
-    assert L.rt_abi_version() == rtow.ABI_VERSION == 3
+    assert L.rt_abi_version() == rtow.ABI_VERSION == 4
     with pytest.raises(rtow.RTError):
         rtow.camera_cpu(aspect=0.0)
 

@@ -12,7 +12,7 @@ import os
 import numpy as np
 import pytest
 
-from oracle_lib import (golden_ppm, golden_scene_rows, golden_stats, kernel_render,
+from oracle_lib import (golden_ppm, golden_scene_rows, golden_stats, kernel_render, kernel_render_exact,
                         ppm_p3_bytes, read_ppm_bytes, reference_render, reference_scene)
 
 C0 = dict(width=400, aspect=16.0 / 9.0, spp=10)
@@ -243,3 +243,40 @@ def test_src_gpu_scene_of_the_gallery_run(rtow):
     r = Xorwow(0)
     u = [r.random_float() for _ in range(10000)]
     assert min(u) >= 0.0 and max(u) < 1.0
+
+
+def _levels(sums, spp):
+    """write_color's level before the int() (src/cpu/color.h:8-23), as a real number."""
+    return 256.0 * np.sqrt(np.clip(sums / spp, 0.0, None))
+
+
+@pytest.mark.parametrize("spp", [1 << 12, 1 << 20])
+def test_sum_format_unbiased_at_high_spp(rtow, spp):
+    """The fixed-point pixel sums against an fp64 sum of
+    the same samples (the reference's accumulation, src/cpu/main.cc:114-119)
+    at 4096 and 2^20 spp, where F = 19 and 11: with the stochastic rounding
+    every pixel's level is within 0.05 of the fp64 one (unbiased; the rounding
+    noise is ~1e-6 level), while plain truncation (the round-2 format) loses
+    up to 2^-F per sample and its darkest pixels drift by more than the bound
+    at 2^20 spp.  The five-sphere book scene (archive-gpu/image22) with its
+    albedos darkened 10x, 8x2 pixels over its darkest rows, keeps the sample
+    count CPU-sized."""
+    scene = rtow.five_scene()
+    scene.albedo = (scene.albedo * 0.1).astype(np.float32)
+    cam = rtow.camera_gpu(8, 4, lookfrom=(-2, 2, 1), lookat=(0, 0, -1), vfov=90.0, defocus_angle=0.0,
+                          focus_dist=3.4)
+    p = rtow.make_params(8, 4, spp, seed=7, flags=rtow.RT_FLAG_GPU_SEMANTICS)
+    p.local_rows = 2  # the two bottom rows are the darkest (under the spheres)
+    p.row_block = 2
+    p.band_stride = 2
+    p.band_offset = 1
+    got, exact, _ = kernel_render_exact(scene, cam, p)
+    lv_got, lv_ex = _levels(got.astype(np.float64), spp), _levels(exact, spp)
+    assert np.all(np.abs(lv_got - lv_ex) <= 0.05), np.abs(lv_got - lv_ex).max()
+    assert abs(float((lv_got - lv_ex).mean())) <= 0.01
+    trunc, exact2, _ = kernel_render_exact(scene, cam, p, no_dither=True)
+    assert np.array_equal(exact, exact2)  # the same samples
+    drift = lv_ex - _levels(trunc.astype(np.float64), spp)
+    assert np.all(drift >= 0)  # truncation only ever loses
+    if spp == 1 << 20:
+        assert drift.max() > 0.05

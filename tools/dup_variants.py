@@ -14,7 +14,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "ray-tracing-in-one-weekend_amd", "csrc", "rt_render.hip")
+SRC = os.path.join(ROOT, "ray-tracing-in-one-weekend_amd", "csrc", "rt_kernel.hip")
 
 EDITS = {
     # the ray-box slab test of every BVH node visit
@@ -155,7 +155,7 @@ def main():
             s = s.replace(old, new)
         d = os.path.join(out, "src_dup_" + part)
         os.makedirs(d, exist_ok=True)
-        p = os.path.join(d, "rt_render.hip")
+        p = os.path.join(d, "rt_kernel.hip")
         open(p, "w").write(s)
         subprocess.run([os.path.join(ROOT, "tools", "build_variant.sh"), "dup_" + part, p], check=True)
         print("built", f"dup_{part}.so")

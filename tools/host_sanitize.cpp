@@ -35,10 +35,17 @@ struct scene {
 };
 
 static void accel(const rt_scene_view &v, bool expect_layer) {
-  uint64_t info[16];
-  CHECK(rt_internal_accel_info(&v, info) == RT_OK);
-  CHECK((info[2] != 0) == expect_layer);
-  if (info[7]) CHECK(info[11] == 1 && info[12] == 1 && info[10] <= 15);
+  // every grid placement (auto, LDS, cells in LDS, global) and a few cell scales
+  for (int place = 0; place <= 3; ++place)
+    for (double scale : {0.0, 0.5, 1.3}) {
+      uint64_t info[RT_ACCEL_INFO_N];
+      CHECK(rt_internal_accel_info(&v, place, scale, info, RT_ACCEL_INFO_N) == RT_OK);
+      CHECK((info[2] != 0) == expect_layer);
+      if (info[7]) CHECK(info[11] == 1 && info[12] == 1 && info[10] <= 15 && info[16] >= 1);
+    }
+  uint64_t two[2];
+  CHECK(rt_internal_accel_info(&v, 0, 0.0, two, 2) == RT_OK);  // a short buffer is filled, no more
+  CHECK(rt_internal_accel_info(&v, 4, 0.0, two, 2) != RT_OK);
 }
 
 int main() {
@@ -75,9 +82,9 @@ int main() {
       s.kind[i] = RT_LAMBERTIAN;
       s.alb[3 * i] = s.alb[3 * i + 1] = s.alb[3 * i + 2] = 0.5f;
     }
-    uint64_t info[16];
+    uint64_t info[RT_ACCEL_INFO_N];
     const rt_scene_view v = s.view(300);
-    CHECK(rt_internal_accel_info(&v, info) == RT_OK);
+    CHECK(rt_internal_accel_info(&v, 0, 0.0, info, RT_ACCEL_INFO_N) == RT_OK);
     if (info[7]) CHECK(info[11] == 1 && info[12] == 1 && info[10] <= 15);
   }
   // cameras (both models, with and without a lens)

@@ -12,10 +12,12 @@ mkdir -p $OUT
 HSAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined"
 FLAGS="--offload-arch=gfx950 -std=c++17 -fPIC -g -O1 -fno-omit-frame-pointer -I$ROOT/include -I$PKG/csrc"
 HIPCC=/opt/rocm/bin/hipcc
-$HIPCC $FLAGS -ffp-contract=off $HSAN -c -o $OUT/rt_render.o $PKG/csrc/rt_render.hip
+$HIPCC $FLAGS -ffp-contract=off $HSAN -c -o $OUT/rt_kernel.o $PKG/csrc/rt_kernel.hip
+$HIPCC $FLAGS $HSAN -c -o $OUT/rt_api.o $PKG/csrc/rt_api.cpp
+$HIPCC $FLAGS $HSAN -c -o $OUT/rt_accel.o $PKG/csrc/rt_accel.cpp
 $HIPCC $FLAGS $HSAN -c -o $OUT/rt_sched.o $PKG/csrc/rt_sched.hip
 $HIPCC $FLAGS $HSAN -x c++ -c -o $OUT/rt_host.o $PKG/csrc/rt_host.cpp
 $HIPCC $FLAGS $HSAN -x c++ -c -o $OUT/driver.o $ROOT/tools/host_sanitize.cpp
-$HIPCC --offload-arch=gfx950 $HSAN -o $OUT/host_sanitize $OUT/driver.o $OUT/rt_host.o $OUT/rt_render.o \
+$HIPCC --offload-arch=gfx950 $HSAN -o $OUT/host_sanitize $OUT/driver.o $OUT/rt_host.o $OUT/rt_kernel.o $OUT/rt_api.o $OUT/rt_accel.o \
   $OUT/rt_sched.o -lpthread
 ASAN_OPTIONS=detect_leaks=1 UBSAN_OPTIONS=print_stacktrace=1 $OUT/host_sanitize
