@@ -131,20 +131,90 @@ def cpu_baseline(spp, procs):
             "seconds": round(dt, 3), "sample": sample + ", single thread (oracle fp64 restatement)"}
 
 
-def load_pmc(workload, accel="scan"):
-    """The committed rocprofv3 PMC summary of this workload (tools/pmc_traffic.py):
-    HBM bytes and VALU wave-instructions per launch; {} if none matches."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json" if accel == "scan"
-                        else f"pmc_traffic_{accel}.json")
+def load_pmc(workload, accel="scan", world=1):
+    """The committed rocprofv3 PMC summary of this workload AND this rank share
+    (tools/pmc_traffic.py; profiles/pmc_traffic_<accel>.json for the whole
+    frame, pmc_traffic_<accel>_w<N>.json for rank 0's 1/N share): HBM bytes and
+    VALU wave-instructions per launch.  Returns (summary or {}, reason)."""
+    name = "pmc_traffic.json" if accel == "scan" else f"pmc_traffic_{accel}.json"
+    if world > 1:
+        name = name.replace(".json", f"_w{world}.json")
+    path = os.path.join(ROOT, "profiles", name)
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("workload") == workload:
-            d["path"] = path
-            return d
     except (OSError, ValueError):
-        pass
-    return {}
+        return {}, f"no committed PMC summary for a {world}-way share ({name})"
+    if d.get("workload") != workload:
+        return {}, f"{name} was collected on another workload ({d.get('workload')!r})"
+    if int(d.get("world", 1)) != world:
+        return {}, f"{name} was collected on a {d.get('world', 1)}-way share, this line is {world}-way"
+    d["path"] = path
+    return d, None
+
+
+def roofline(work, k_avg_s, accel, pmc, pmc_reason, device_sha):
+    """The `roofline` object of the JSON line.  work: executed work of one launch
+    (RT_FLAG_COUNT_WORK counters of this rank's share); k_avg_s: this run's
+    average render time of that share; pmc: the committed PMC summary of the
+    SAME share (load_pmc), or {} -- then every counter-derived field is null
+    and `pmc_null_reason` says why (counters of another share divided by this
+    share's time would be meaningless)."""
+    # box_tests counts slab tests (layer BVH) or DDA cell steps (layer grid)
+    flops = work["sphere_tests"] * FLOPS_PER_TEST + work["box_tests"] * (
+        FLOPS_PER_CELL if accel == "bvh" else FLOPS_PER_BOX)
+    achieved = flops / k_avg_s / 1e12
+    # the counters are only valid for the device code they were collected on
+    pmc_fresh = bool(pmc) and pmc.get("device_code_sha16") == device_sha
+    valu_insts = pmc.get("valu_insts_per_launch")
+    cnt = pmc.get("counters_avg_per_dispatch", {})
+    traffic = pmc.get("hbm_bytes_per_launch")
+    clock_ghz = (cnt["GRBM_GUI_ACTIVE"] / N_XCD / k_avg_s / 1e9) if cnt.get("GRBM_GUI_ACTIVE") else None
+    valu_issue = None
+    if valu_insts:
+        rate = valu_insts / k_avg_s
+        valu_issue = {"achieved": round(rate / 1e9, 1), "unit": "G wave-instr/s",
+                      "source": "SQ_INSTS_VALU per launch (committed PMC summary of this share) / this "
+                                "run's kernel time"}
+        if clock_ghz:
+            peak2 = N_SIMD * clock_ghz * 1e9 / 2  # one wave64 VALU instruction per 2 cycles per SIMD
+            valu_issue.update({"peak": round(peak2 / 1e9, 1), "frac": round(rate / peak2, 3),
+                               "clock_ghz": round(clock_ghz, 3),
+                               "peak_basis": "wave64 VALU issue every 2 cycles per SIMD "
+                                             "(MI355X_MICROARCH.md) x 1024 SIMDs at the clock from "
+                                             "GRBM_GUI_ACTIVE / 8 XCDs / kernel time"})
+        valu_issue.update({"peak_ubench": round(VALU_ISSUE_PEAK / 1e9, 1),
+                           "frac_ubench": round(rate / VALU_ISSUE_PEAK, 3),
+                           "peak_ubench_basis": "dependency-free v_fma_f32 stream, 1.041 ns per "
+                                                "wave instruction per SIMD (tools/ubench_exec.hip)"})
+    lane_util = None
+    if cnt.get("SQ_THREAD_CYCLES_VALU") and cnt.get("SQ_ACTIVE_INST_VALU"):
+        lane_util = round(cnt["SQ_THREAD_CYCLES_VALU"] / (64.0 * cnt["SQ_ACTIVE_INST_VALU"]), 3)
+    return {"bound": "valu", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
+            "traffic": traffic,
+            "achieved_basis": "executed work per launch (RT_FLAG_COUNT_WORK frame of this rank's share): "
+                              "ray-sphere tests x 17 flop + grid cell steps x 2 flop "
+                              "(layer BVH: box tests x 12) / HIP-event kernel time",
+            "valu_issue": valu_issue,
+            "valu_lane_util": lane_util,
+            "valu_lane_util_basis": "SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU): "
+                                    "mean active lanes per VALU instruction / 64",
+            "hbm": ({"achieved_GBps": round(traffic / k_avg_s / 1e9, 1),
+                     "peak_GBps": PEAK_HBM_GBPS,
+                     "frac": round(traffic / k_avg_s / 1e9 / PEAK_HBM_GBPS, 5)}
+                    if traffic else None),
+            "pmc_source": os.path.relpath(pmc["path"], ROOT) if pmc.get("path") else None,
+            "pmc_matches_device_code": pmc_fresh,
+            "pmc_null_reason": pmc_reason,
+            "culling_speedup": round(work["bf_tests"] / max(1, work["sphere_tests"]), 1),
+            "culling_speedup_basis": "brute-force ray-sphere tests (segments x spheres, "
+                                     "SURVEY 8d) / tests the walk executes; not a roofline "
+                                     "fraction",
+            "note": "fp32 VALU-bound (no MFMA, HBM idle): the kernel is control-heavy "
+                    "(compares, selects, branches, divergent per-lane walks), so "
+                    "valu_issue and valu_lane_util say how close it runs to the issue "
+                    "ceiling; frac counts only the algorithmic flops"}
 
 
 def main():
@@ -219,8 +289,12 @@ def main():
             events[1].record(stream)
         ctx.tonemap_async(tile.data_ptr(), params.local_rows * W, max(spp, 1), tile_u8.data_ptr(),
                           rtow.RT_TONEMAP_CPU, stream.cuda_stream)
+        if events is not None:
+            events[2].record(stream)
         if world > 1:
             dist.gather(tile_u8 if a.backend == "nccl" else tile_u8.cpu(), gather_list, dst=0)
+        if events is not None:
+            events[3].record(stream)
 
     assert stream.cuda_stream != 0
     first_frame_ms = None
@@ -238,8 +312,7 @@ def main():
             if i == 0:
                 first_frame_ms = (time.perf_counter() - t_first) * 1e3
         ctx.reset_stats(stream.cuda_stream)
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(a.steps)]
+        evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(4)) for _ in range(a.steps)]
 
         barrier()
         torch.cuda.synchronize(dev)
@@ -253,7 +326,9 @@ def main():
     sums_last, u8_last = tile.cpu().numpy(), tile_u8.cpu().numpy()
 
     st = ctx.collect_stats()
-    kernel_ms = [e0.elapsed_time(e1) for e0, e1 in evs]
+    kernel_ms = [e[0].elapsed_time(e[1]) for e in evs]
+    tonemap_ms = [e[1].elapsed_time(e[2]) for e in evs]
+    gather_ms = [e[2].elapsed_time(e[3]) for e in evs]
     # executed work per launch: one instrumented frame (RT_FLAG_COUNT_WORK build),
     # same seed as timed step 0, outside the timed region
     wp = rtow_dist.partition(W, H, spp, world, rank, a.row_block, max_depth=a.depth,
@@ -265,12 +340,15 @@ def main():
     work = ctx.collect_stats()
     local = torch.tensor([float(st.segments), float(st.samples), float(st.wave_steps)],
                          dtype=torch.float64, device=gdev)
-    t_max = torch.tensor([elapsed], dtype=torch.float64, device=gdev)
+    mean = lambda v: sum(v) / len(v)
+    # max over ranks: the wall time, and each part of the step (render, write_color, gather)
+    t_max = torch.tensor([elapsed, mean(kernel_ms), mean(tonemap_ms), mean(gather_ms)], dtype=torch.float64,
+                         device=gdev)
     if world > 1:
         dist.all_reduce(local, op=dist.ReduceOp.SUM)
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     segments, samples, wave_steps = local.tolist()
-    elapsed = float(t_max.item())
+    elapsed, render_ms_max, tonemap_ms_max, gather_ms_max = t_max.tolist()
 
     if rank == 0:
         # assemble the last frame on rank 0 (outside the timed region) and sanity-check it
@@ -285,37 +363,10 @@ def main():
             rtow.write_ppm(a.out, frame, binary=a.out.endswith((".p6", ".pnm")))
 
         k_avg_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-        # box_tests counts slab tests (layer BVH) or DDA cell steps (layer grid)
-        flops = work.sphere_tests * FLOPS_PER_TEST + work.box_tests * (
-            FLOPS_PER_CELL if a.accel == "bvh" else FLOPS_PER_BOX)
-        achieved = flops / k_avg_s / 1e12
         value = segments / elapsed / 1e6
-        pmc = load_pmc(workload, a.accel)
-        # the counters are only valid for the device code they were collected on
-        pmc_fresh = bool(pmc) and pmc.get("device_code_sha16") == rtow.device_code_sha16()
-        valu_insts = pmc.get("valu_insts_per_launch")
-        cnt = pmc.get("counters_avg_per_dispatch", {})
-        traffic = pmc.get("hbm_bytes_per_launch")
-        clock_ghz = (cnt["GRBM_GUI_ACTIVE"] / N_XCD / k_avg_s / 1e9) if cnt.get("GRBM_GUI_ACTIVE") else None
-        valu_issue = None
-        if valu_insts:
-            rate = valu_insts / k_avg_s
-            valu_issue = {"achieved": round(rate / 1e9, 1), "unit": "G wave-instr/s",
-                          "source": "SQ_INSTS_VALU per launch (committed PMC summary) / this run's kernel time"}
-            if clock_ghz:
-                peak2 = N_SIMD * clock_ghz * 1e9 / 2  # one wave64 VALU instruction per 2 cycles per SIMD
-                valu_issue.update({"peak": round(peak2 / 1e9, 1), "frac": round(rate / peak2, 3),
-                                   "clock_ghz": round(clock_ghz, 3),
-                                   "peak_basis": "wave64 VALU issue every 2 cycles per SIMD "
-                                                 "(MI355X_MICROARCH.md) x 1024 SIMDs at the clock from "
-                                                 "GRBM_GUI_ACTIVE / 8 XCDs / kernel time"})
-            valu_issue.update({"peak_ubench": round(VALU_ISSUE_PEAK / 1e9, 1),
-                               "frac_ubench": round(rate / VALU_ISSUE_PEAK, 3),
-                               "peak_ubench_basis": "dependency-free v_fma_f32 stream, 1.041 ns per "
-                                                    "wave instruction per SIMD (tools/ubench_exec.hip)"})
-        lane_util = None
-        if cnt.get("SQ_THREAD_CYCLES_VALU") and cnt.get("SQ_ACTIVE_INST_VALU"):
-            lane_util = round(cnt["SQ_THREAD_CYCLES_VALU"] / (64.0 * cnt["SQ_ACTIVE_INST_VALU"]), 3)
+        pmc, pmc_reason = load_pmc(workload, a.accel, world)
+        roof = roofline({"sphere_tests": work.sphere_tests, "box_tests": work.box_tests,
+                         "bf_tests": work.bf_tests}, k_avg_s, a.accel, pmc, pmc_reason, rtow.device_code_sha16())
         out = {
             "metric": "Mray/s (ray segments = closest-hit queries per second), final random-spheres "
                       "scene 3840x2160 @ 500spp depth 50" if not a.preset or a.preset == "c2"
@@ -354,31 +405,20 @@ def main():
             "first_frame_note": "wall time of the first frame of this geometry on its own, pilot schedule "
                                 "included (4-spp pilot + device sort of the tile order); ms_per_step "
                                 "reuses the order",
-            "roofline": {"bound": "valu", "achieved": round(achieved, 2), "peak": PEAK_FP32_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                         "traffic": traffic,
-                         "achieved_basis": "executed work per launch (RT_FLAG_COUNT_WORK frame): "
-                                           "ray-sphere tests x 17 flop + grid cell steps x 2 flop "
-                                           "(layer BVH: box tests x 12) / HIP-event kernel time",
-                         "valu_issue": valu_issue,
-                         "valu_lane_util": lane_util,
-                         "valu_lane_util_basis": "SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU): "
-                                                 "mean active lanes per VALU instruction / 64",
-                         "hbm": ({"achieved_GBps": round(traffic / k_avg_s / 1e9, 1),
-                                  "peak_GBps": PEAK_HBM_GBPS,
-                                  "frac": round(traffic / k_avg_s / 1e9 / PEAK_HBM_GBPS, 5)}
-                                 if traffic else None),
-                         "pmc_source": os.path.relpath(pmc["path"], ROOT) if pmc.get("path") else None,
-                         "pmc_matches_device_code": pmc_fresh,
-                         "culling_speedup": round(work.bf_tests / max(1, work.sphere_tests), 1),
-                         "culling_speedup_basis": "brute-force ray-sphere tests (segments x spheres, "
-                                                  "SURVEY 8d) / tests the walk executes; not a roofline "
-                                                  "fraction",
-                         "note": "fp32 VALU-bound (no MFMA, HBM idle): the kernel is control-heavy "
-                                 "(compares, selects, branches, divergent per-lane walks), so "
-                                 "valu_issue and valu_lane_util say how close it runs to the issue "
-                                 "ceiling; frac counts only the algorithmic flops"},
+            "step_parts_ms": {"render_max_over_ranks": round(render_ms_max, 3),
+                              "write_color_max_over_ranks": round(tonemap_ms_max, 3),
+                              "gather_max_over_ranks": round(gather_ms_max, 3),
+                              "basis": "HIP events on each rank's launch stream around its render, "
+                                       "its device write_color and the RCCL gather of the byte tiles "
+                                       "(0 at N = 1); mean over the timed steps, max over ranks"},
+            "roofline": roof,
+            "cpu_baseline": None,
+            "cpu_baseline_note": None if world == 1 else
+                                 "measured at N = 1 only (rank 0's host cores would be shared with "
+                                 "N render processes); see the N = 1 line",
         }
+        if world == 1 and a.no_cpu_baseline:
+            out["cpu_baseline_note"] = "skipped (--no-cpu-baseline)"
         if world == 1 and not a.no_cpu_baseline:
             try:
                 procs = a.cpu_procs or min(16, os.cpu_count() or 1)

@@ -154,7 +154,11 @@ int main(int argc, char **argv) {
   int ndev = 0;
   check(rt_device_count(&ndev), "rt_device_count");
   if (ndev < 1) die("no HIP device", RT_ERR_NO_DEVICE);
-  if (o.gpus > ndev) o.gpus = ndev;
+  if (o.gpus > ndev) {
+    // no silent clamp: a run asked for N GPUs must not report a 1-GPU time as N
+    std::fprintf(stderr, "rtow: --gpus %d but only %d HIP device(s) visible\n", o.gpus, ndev);
+    std::exit(2);
+  }
 
   // the reference's stderr surface, per personality (src/cpu/main.cc:103-105,
   // src/gpu/main.cu:121-125); our extra lines follow the timing
@@ -242,15 +246,24 @@ int main(int argc, char **argv) {
     if (use_rccl && g == 0 && hipMalloc(&d_all, 3 * tile_px * o.gpus) != hipSuccess)
       die("gather buffer", RT_ERR_HIP);
   }
+  // per device: events before the render, after it, after write_color and
+  // after the gather, for the per-device lines on stderr
+  std::vector<hipEvent_t> ev(4 * (size_t)o.gpus, nullptr);
   for (int g = 0; g < o.gpus; ++g) {
     (void)hipSetDevice(devs[g]);
+    for (int k = 0; k < 4; ++k)
+      if (hipEventCreate(&ev[4 * g + k]) != hipSuccess) die("hipEventCreate", RT_ERR_HIP);
     (void)hipDeviceSynchronize();
   }
   const auto start = std::chrono::high_resolution_clock::now();
   for (int g = 0; g < o.gpus; ++g) {
+    (void)hipSetDevice(devs[g]);
+    (void)hipEventRecord(ev[4 * g + 0], streams[g]);
     check(rt_render_async(ctxs[g], &cam, &jobs[g].params, d_tile[g], streams[g]), "rt_render_async");
+    (void)hipEventRecord(ev[4 * g + 1], streams[g]);
     check(rt_tonemap_async(ctxs[g], d_tile[g], tile_px, o.spp > 0 ? o.spp : 1, tone_mode, d_u8[g], streams[g]),
           "rt_tonemap_async");
+    (void)hipEventRecord(ev[4 * g + 2], streams[g]);
   }
   if (use_rccl) {
     if (ncclGroupStart() != ncclSuccess) die("ncclGroupStart", RT_ERR_HIP);
@@ -259,6 +272,10 @@ int main(int argc, char **argv) {
           ncclSuccess)
         die("ncclGather", RT_ERR_HIP);
     if (ncclGroupEnd() != ncclSuccess) die("ncclGroupEnd", RT_ERR_HIP);
+  }
+  for (int g = 0; g < o.gpus; ++g) {
+    (void)hipSetDevice(devs[g]);
+    (void)hipEventRecord(ev[4 * g + 3], streams[g]);
   }
   for (int g = 0; g < o.gpus; ++g) {
     (void)hipSetDevice(devs[g]);
@@ -296,6 +313,18 @@ int main(int argc, char **argv) {
     std::fprintf(stderr, "Number of GPUs = %d, spheres = %u\n", o.gpus, buf.n);
     std::fprintf(stderr, "Throughput = %.1f Mray/s, %.1f Msample/s (%llu segments)\n",
                  segs / (ms * 1e3), samples / (ms * 1e3), segs);
+    // per device: render (its launches), write_color, and the wait for the
+    // gather (the RCCL gather of the byte tiles ends on every device's stream)
+    for (int g = 0; g < o.gpus; ++g) {
+      float r = 0.f, t = 0.f, x = 0.f;
+      (void)hipSetDevice(devs[g]);
+      (void)hipEventElapsedTime(&r, ev[4 * g + 0], ev[4 * g + 1]);
+      (void)hipEventElapsedTime(&t, ev[4 * g + 1], ev[4 * g + 2]);
+      (void)hipEventElapsedTime(&x, ev[4 * g + 2], ev[4 * g + 3]);
+      std::fprintf(stderr, "GPU %d (device %d): render %.3f ms in %llu launch(es), write_color %.3f ms, %s %.3f ms\n",
+                   g, devs[g], r, (unsigned long long)jobs[g].stats.launches, t,
+                   use_rccl ? "gather (RCCL)" : "gather (none)", x);
+    }
   }
 
   // ---- assemble rows + PPM (output_image, src/gpu/camera.h:197-210) ----
@@ -320,6 +349,7 @@ int main(int argc, char **argv) {
   if (fd != 1) ::close(fd);
   for (int g = 0; g < o.gpus; ++g) {
     (void)hipSetDevice(devs[g]);
+    for (int k = 0; k < 4; ++k) (void)hipEventDestroy(ev[4 * g + k]);
     (void)hipFree(d_tile[g]);
     (void)hipFree(d_u8[g]);
     (void)hipStreamDestroy(streams[g]);

@@ -965,7 +965,15 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         float rx, ry, rz;
         reflect3(dx, dy, dz, nx, ny, nz, dn, rx, ry, rz);
         float sx, sy, sz;
-        bool scattered = true;
+        // An opaque sphere hit from inside (DESIGN.md 2, step 4): the path got
+        // in past the surface within t_min of a contact point (a glass sphere
+        // resting on the ground: src/cpu does the same, main.cc:19) and can
+        // never leave -- every lambertian or metal scatter off an inner wall
+        // points inward -- so it ends black here, as it would at the depth cap,
+        // without tracing the rest inside (segments of up to 2000 units from
+        // origins beyond the grid's padding bound, each a whole-scene scan:
+        // C4's rank share 408 -> 143 ms at 100 spp, profiles/r03d_c4_ab.log)
+        bool scattered = front;
         if (sr.kind == RT_LAMBERTIAN) {
           // material.h:19-30
           sx = nx + ux;
@@ -984,13 +992,14 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           sx = fmaf(fz, ux, rx);
           sy = fmaf(fz, uy, ry);
           sz = fmaf(fz, uz, rz);
-          scattered = dot3(sx, sy, sz, nx, ny, nz) > 0.0f;
+          scattered = scattered && dot3(sx, sy, sz, nx, ny, nz) > 0.0f;
         } else {
           // dielectric, material.h:57-87 (r0 is the same for ior and 1/ior)
           const float ratio = front ? sr.inv_param : sr.param;
           const float cos_t = fminf(-dn, 1.0f);
           // ratio sin > 1 (material.h:64), squared: no square root
           const bool cannot = (ratio * ratio) * fmaf(-cos_t, cos_t, 1.0f) > 1.0f;
+          scattered = true;  // a dielectric is entered and left
           if (cannot || schlick(cos_t, sr.r0) > unif(r.x)) {
             sx = rx;
             sy = ry;
@@ -999,14 +1008,6 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
             refract3(dx, dy, dz, nx, ny, nz, cos_t, ratio, sx, sy, sz);
           }
         }
-        // An opaque sphere hit from inside (DESIGN.md 2, step 4): the path got
-        // in past the surface within t_min of a contact point (a glass sphere
-        // resting on the ground: src/cpu does the same, main.cc:19) and can
-        // never leave -- every lambertian or metal scatter off an inner wall
-        // points inward -- so it ends black here, as it would at the depth cap,
-        // without tracing the rest inside (segments of up to 2000 units from
-        // origins beyond the grid's padding bound, each a whole-scene scan)
-        scattered = scattered && (front || sr.kind == RT_DIELECTRIC);
         // attenuation = albedo (dielectrics store 1,1,1: the product is exact)
         thr *= sr.ar;
         thg *= sr.ag;

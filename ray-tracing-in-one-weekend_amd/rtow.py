@@ -139,7 +139,8 @@ def lib():
                                    ctypes.c_int]
         L.rt_internal_accel_info.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double,
                                              ctypes.c_void_p, ctypes.c_size_t]
-        L.rt_context_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
+        if hasattr(L, "rt_context_set_option"):  # (absent in pre-ABI-4 builds loaded for A/B runs)
+            L.rt_context_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
         _lib = L
     return _lib
 

@@ -309,6 +309,26 @@ def test_cli_rccl_gather_path_prints_the_same_ppm():
     assert a == b
 
 
+def test_cli_reports_each_device_and_refuses_missing_gpus(rtow):
+    """gpu_ray_tracer prints one stderr line per device (render ms and its
+    launch count, write_color ms, gather ms) after the reference's timing
+    lines, and refuses --gpus N beyond the visible devices (exit 2) instead of
+    rendering on fewer and reporting the time as N GPUs' (VERDICT r2, item 7)."""
+    import os
+    import re
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "..", "ray-tracing-in-one-weekend_amd", "bin", "gpu_ray_tracer")
+    args = [exe, "--width", "96", "--height", "54", "--spp", "8", "--seed", "5", "--out", os.devnull]
+    r = subprocess.run(args + ["--gather", "rccl"], capture_output=True, timeout=120, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Time Cost (ms) = " in r.stderr
+    assert re.search(r"GPU 0 \(device 0\): render [0-9.]+ ms in 1 launch\(es\), write_color [0-9.]+ ms, "
+                     r"gather \(RCCL\) [0-9.]+ ms", r.stderr), r.stderr
+    n = rtow.device_count()
+    bad = subprocess.run(args + ["--gpus", str(n + 1)], capture_output=True, timeout=120, text=True)
+    assert bad.returncode == 2 and f"only {n} HIP device" in bad.stderr
+
+
 def test_scene_upload_rejects_non_finite_centres(rtow, gpu_ctx):
     s = rtow.final_scene()
     cx = s.cx.copy()

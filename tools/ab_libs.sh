@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 run() {
   local lib=ray-tracing-in-one-weekend_amd/librtow.so
   [ "$1" != base ] && lib=build/variants/$1.so
-  RTOW_LIB=$lib timeout -k 10 90 python tools/ab_flags.py --reps 2 ${AB_FLAGS:-ACCEL_BVH+PILOT_SCHEDULE} | sed "s/^/$1 /"
+  RTOW_LIB=$lib timeout -k 10 90 python tools/ab_flags.py --reps ${REPS:-2} ${AB_FLAGS:-ACCEL_BVH+PILOT_SCHEDULE} | sed "s/^/$1 /"
 }
 run base
 for v in "$@"; do run $v; done

@@ -32,6 +32,9 @@ def main():
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--kernel", default="render_kernel")
     ap.add_argument("--workload", default="")
+    ap.add_argument("--world", type=int, default=1,
+                    help="the rank share profiled: 1 = the whole frame, N = rank 0's 1/N share "
+                         "(bench.py matches a line's world against it)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     # only the full-size dispatches of the kernel: the bench also launches it on
@@ -58,13 +61,15 @@ def main():
         v = sorted(v[1:] if len(v) > 1 else v)
         return v[len(v) // 2] if len(v) % 2 else 0.5 * (v[len(v) // 2 - 1] + v[len(v) // 2])
     avg = {k: steady(v) for k, v in vals.items()}
-    out = {"kernel": a.kernel, "workload": a.workload, "grid_size": grid, "counters_avg_per_dispatch": avg,
+    out = {"kernel": a.kernel, "workload": a.workload, "world": a.world, "grid_size": grid,
+           "counters_avg_per_dispatch": avg,
            "dispatches": {k: len(v) for k, v in vals.items()},
            "per_dispatch": dict(vals), "statistic": "median over full-size dispatches after the first (warmup)", "device_code_sha16": rtow.device_code_sha16()}
     g = [dur[k] for k in dur if k[0] == "GRBM_GUI_ACTIVE"]
     if "GRBM_GUI_ACTIVE" in avg and g:
         # GRBM_GUI_ACTIVE is summed over the 8 XCDs
         out["clock_ghz_pmc_pass"] = round(avg["GRBM_GUI_ACTIVE"] / 8 / (sum(g) / len(g)) / 1e9, 3)
+        out["kernel_s_pmc_pass"] = sum(g) / len(g)  # mean dispatch duration in that pass
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         out["fetch_bytes"] = avg["FETCH_SIZE"] * 1024
         out["write_bytes"] = avg["WRITE_SIZE"] * 1024
