@@ -626,6 +626,268 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
   return segs;
 }
 
+// ---------------------------------------------------------------------
+// src/gpu restatement (rto_gpuref_render): the reference CUDA path's own
+// per-sample arithmetic, fp32, as src/gpu/camera.h:112-195, sphere.h:15-44,
+// material.h:20-104 and rtweekend.h:42-69 write it -- for attributing the
+// brightness difference between the kernel specification (GPU semantics
+// flags) and gallery/gpu/image23.png.  Each switch replaces one
+// part of the kernel specification with src/gpu's form:
+//   GREF_NAIVE_HIT: sphere::hit's quadratic (oc = O - C, a = |d|^2, roots
+//                   (-half_b -+ sqrt(disc)) / a, the open interval, the scan's
+//                   shrinking t_max), hit point O + t d, set_face_normal by
+//                   dot(d, outward) -- no refinement, no spurious-root rule, no
+//                   opaque-inside rule;
+//   GREF_UNNORM:    directions left unnormalised (the camera's pixel_sample -
+//                   origin, scatter directions as built), unit_vector(d) =
+//                   d (1 / |d|) where src/gpu takes one (needs GREF_NAIVE_HIT:
+//                   the kernel's quadratic assumes |d| = 1);
+//   GREF_REJECT:    random_in_unit_sphere / random_in_unit_disk by rejection
+//                   (random_unit_vector = its unit_vector), uniforms from
+//                   pcg4d batches of 4;
+//   GREF_FP32_SUM:  pixel sums in fp32 (camera.h:189-194) instead of the
+//                   fixed-point sums.
+// nvcc contracts a*b+c into fma by default (-fmad=true): the dot products and
+// o + t d are written as fma chains.  Uniforms come from pcg4d (src/gpu draws
+// curand XORWOW): equal in distribution, a different stream.
+enum { GREF_NAIVE_HIT = 1, GREF_UNNORM = 2, GREF_REJECT = 4, GREF_FP32_SUM = 8 };
+
+struct gvec {
+  float x, y, z;
+};
+inline gvec gadd(gvec a, gvec b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline gvec gsub(gvec a, gvec b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline gvec gmul(float t, gvec v) { return {t * v.x, t * v.y, t * v.z}; }
+inline float gdot(gvec a, gvec b) { return fmaf_(a.z, b.z, fmaf_(a.y, b.y, a.x * b.x)); }
+inline gvec gfma(float t, gvec d, gvec o) { return {fmaf_(t, d.x, o.x), fmaf_(t, d.y, o.y), fmaf_(t, d.z, o.z)}; }
+inline gvec gunit(gvec v) { return gmul(1.0f / std::sqrt(gdot(v, v)), v); }  // vec3.h: v / length, operator/ = (1/t) v
+
+// a stream of uniforms for one (pixel, sample, bounce): pcg4d batches
+struct gdraws {
+  uint32_t pix, sample, slot, seed, batch = 0, k = 4;
+  u4 cur{};
+  float next() {
+    if (k == 4) {
+      cur = pcg4d(pix, sample, slot | (batch++ << 16), seed);
+      k = 0;
+    }
+    const uint32_t v[4] = {cur.x, cur.y, cur.z, cur.w};
+    return unif(v[k++]);
+  }
+};
+
+gvec g_in_unit_sphere(gdraws &r) {  // rtweekend.h:42-49
+  while (true) {
+    const float x = fmaf_(2.0f, r.next(), -1.0f), y = fmaf_(2.0f, r.next(), -1.0f), z = fmaf_(2.0f, r.next(), -1.0f);
+    const gvec p{x, y, z};
+    if (gdot(p, p) < 1.0f) return p;
+  }
+}
+
+unsigned long long gpuref_pixel(const kctx &k, int col, int grow, float acc[3], int mode) {
+  const kscene &sc = *k.sc;
+  const rt_camera &c = *k.cam;
+  const uint32_t pix = (uint32_t)grow * (uint32_t)k.p->width + (uint32_t)col;
+  const size_t n = sc.cx.size();
+  const bool naive = mode & GREF_NAIVE_HIT, unnorm = (mode & GREF_UNNORM) && naive, reject = mode & GREF_REJECT;
+  unsigned long long segs = 0;
+  float fsum[3] = {0.0f, 0.0f, 0.0f};
+  uint32_t q[3] = {0u, 0u, 0u};
+  int f = 31;
+  for (int s = k.p->spp; s > 1; s >>= 1) --f;
+  const float qscale = std::ldexp(1.0f, f), qinv = std::ldexp(1.0f, -f);
+  for (uint32_t sample = 0; sample < (uint32_t)k.p->spp; ++sample) {
+    // get_ray (camera.h:153-167): the kernel's camera arithmetic for the
+    // target; the lens by rejection or the polar draw
+    const u4 r0 = pcg4d(pix, sample, 0u, k.seed32);
+    float fs, ft;
+    if (c.model == RT_CAMERA_CPU) {
+      fs = ((float)col + unif(r0.x)) * (float)(1.0 / (k.p->width - 1));
+      ft = ((float)(k.p->height - 1 - grow) + unif(r0.y)) * (float)(1.0 / (k.p->height - 1));
+    } else {
+      fs = (float)col + (unif(r0.x) - 0.5f);
+      ft = (float)grow + (unif(r0.y) - 0.5f);
+    }
+    gvec tgt, o{c.eye[0], c.eye[1], c.eye[2]};
+    tgt.x = fmaf_(ft, c.vert[0], fmaf_(fs, c.horiz[0], c.corner[0]));
+    tgt.y = fmaf_(ft, c.vert[1], fmaf_(fs, c.horiz[1], c.corner[1]));
+    tgt.z = fmaf_(ft, c.vert[2], fmaf_(fs, c.horiz[2], c.corner[2]));
+    if (c.has_lens) {
+      float dx, dy;
+      if (reject) {  // random_in_unit_disk, rtweekend.h:61-69
+        gdraws dr{pix, sample, 0u, k.seed32};
+        dr.k = 2;  // r0's z and w first
+        dr.cur = r0;
+        do {
+          dx = fmaf_(2.0f, dr.next(), -1.0f);
+          dy = fmaf_(2.0f, dr.next(), -1.0f);
+        } while (!(fmaf_(dy, dy, dx * dx) < 1.0f));
+      } else {
+        const float rr = sqrt_k(unif(r0.z));
+        float sn, cs;
+        sincos_turn(unif(r0.w), sn, cs);
+        dx = rr * cs;
+        dy = rr * sn;
+      }
+      o.x = fmaf_(dy, c.lens_v[0], fmaf_(dx, c.lens_u[0], o.x));
+      o.y = fmaf_(dy, c.lens_v[1], fmaf_(dx, c.lens_u[1], o.y));
+      o.z = fmaf_(dy, c.lens_v[2], fmaf_(dx, c.lens_u[2], o.z));
+    }
+    gvec d = gsub(tgt, o);
+    if (!unnorm) normalize3(d.x, d.y, d.z);
+    gvec att{1.0f, 1.0f, 1.0f};
+    gvec col3{0.0f, 0.0f, 0.0f};
+    for (int depth = 0; depth < k.p->max_depth; ++depth) {
+      ++segs;
+      long best = -1;
+      float tbest = INFINITY;
+      gvec p{}, nrm{};
+      bool front = true;
+      if (naive) {
+        // hittable_list::hit (hittable_list.h:49-65) over sphere::hit (sphere.h:15-44)
+        const float a = gdot(d, d);
+        for (size_t i = 0; i < n; ++i) {
+          const gvec oc = gsub(o, gvec{sc.cx[i], sc.cy[i], sc.cz[i]});
+          const float hb = gdot(oc, d);
+          const float cc = fmaf_(-sc.radius[i], sc.radius[i], gdot(oc, oc));
+          const float disc = fmaf_(hb, hb, -(a * cc));
+          if (disc < 0.0f) continue;
+          const float sq = std::sqrt(disc);
+          float root = (-hb - sq) / a;
+          if (!(root > 0.001f && root < tbest)) {  // interval::surrounds
+            root = (-hb + sq) / a;
+            if (!(root > 0.001f && root < tbest)) continue;
+          }
+          tbest = root;
+          best = (long)i;
+        }
+        if (best >= 0) {
+          const size_t b = (size_t)best;
+          p = gfma(tbest, d, o);
+          const gvec outward = gmul(1.0f / sc.radius[b], gsub(p, gvec{sc.cx[b], sc.cy[b], sc.cz[b]}));
+          front = gdot(d, outward) < 0.0f;  // hittable.h:16-19
+          nrm = front ? outward : gvec{-outward.x, -outward.y, -outward.z};
+        }
+      } else {
+        // the kernel specification's closest hit, refinement and shading normal
+        const float nk1 = -dot3(o.x, o.y, o.z, d.x, d.y, d.z);
+        const float o2 = dot3(o.x, o.y, o.z, o.x, o.y, o.z);
+        const float ox2 = -2.0f * o.x, oy2 = -2.0f * o.y, oz2 = -2.0f * o.z;
+        bool near = true;
+        for (size_t i = 0; i < n; ++i) {
+          const float h = fmaf_(sc.cz[i], d.z, fmaf_(sc.cx[i], d.x, fmaf_(sc.cy[i], d.y, nk1)));
+          const float g = fmaf_(sc.cz[i], oz2, fmaf_(sc.cx[i], ox2, fmaf_(sc.cy[i], oy2, o2)));
+          const float e = fmaf_(h, h, -g);
+          if (!(e >= sc.ks[i])) continue;
+          const float sq = sqrt_k(e - sc.ks[i]);
+          const float t0 = h - sq, t1 = h + sq;
+          const bool use0 = t0 > 0.001f;
+          const float root = use0 ? t0 : t1;
+          if (root > 0.001f && (root < tbest || (root == tbest && (long)i < best))) {
+            tbest = root;
+            near = use0;
+            best = (long)i;
+          }
+        }
+        if (best >= 0) {
+          const size_t b = (size_t)best;
+          // refine
+          const float r2 = sc.radius[b] * sc.radius[b];
+          const float ocx = o.x - sc.cx[b], ocy = o.y - sc.cy[b], ocz = o.z - sc.cz[b];
+          const float bb = dot3(ocx, ocy, ocz, d.x, d.y, d.z);
+          float cc;
+          if (r2 < o2 + std::fabs(sc.ks[b])) cc = fmaf_(ocz, ocz, fmaf_(ocy, ocy, fmaf_(ocx, ocx, -r2)));
+          else cc = fmaf_(sc.cz[b], oz2, fmaf_(sc.cy[b], oy2, fmaf_(sc.cx[b], ox2, o2))) + sc.ks[b];
+          float disc;
+          if (r2 < bb * bb) {
+            const float fx = fmaf_(-bb, d.x, ocx), fy = fmaf_(-bb, d.y, ocy), fz = fmaf_(-bb, d.z, ocz);
+            disc = fmaf_(-fz, fz, fmaf_(-fy, fy, fmaf_(-fx, fx, r2)));
+          } else {
+            disc = fmaf_(bb, bb, -cc);
+          }
+          const float sq = sqrt_k(disc);
+          const float qq = -(bb + (bb < 0.0f ? -sq : sq));
+          float t = tbest;
+          if (qq != 0.0f) {
+            const float ta = qq, tb = cc * (1.0f / qq);
+            const float tr = near ? std::fmin(ta, tb) : std::fmax(ta, tb);
+            if (std::isfinite(tr)) t = tr;
+          }
+          if (t < 0.001f && bb > 0.0f) {  // spurious root: move on, not a segment
+            o = gfma(tbest, d, o);
+            --segs;
+            --depth;
+            continue;
+          }
+          p = gfma(t, d, o);
+          nrm = gvec{(p.x - sc.cx[b]) * sc.inv_r[b], (p.y - sc.cy[b]) * sc.inv_r[b], (p.z - sc.cz[b]) * sc.inv_r[b]};
+          front = near != (sc.inv_r[b] < 0.0f);
+          if (!front) nrm = gvec{-nrm.x, -nrm.y, -nrm.z};
+        }
+      }
+      if (best < 0) {  // camera.h:118-124
+        const gvec ud = unnorm ? gunit(d) : d;
+        const float a = 0.5f * (ud.y + 1.0f);
+        const float s0 = 1.0f - a;
+        col3 = gvec{att.x * fmaf_(a, 0.5f, s0), att.y * fmaf_(a, 0.7f, s0), att.z * (s0 + a)};
+        break;
+      }
+      const size_t b = (size_t)best;
+      gdraws dr{pix, sample, (uint32_t)(depth + 1), k.seed32};
+      auto unit_vector = [&]() -> gvec {
+        if (reject) return gunit(g_in_unit_sphere(dr));
+        gvec u;
+        unit_vec(dr.next(), dr.next(), u.x, u.y, u.z);
+        return u;
+      };
+      gvec sd;
+      bool scattered = true;
+      if (sc.kind[b] == RT_LAMBERTIAN) {  // material.h:20-40
+        sd = gadd(nrm, unit_vector());
+        const float e = 1e-8f;
+        if (std::fabs(sd.x) < e && std::fabs(sd.y) < e && std::fabs(sd.z) < e) sd = nrm;
+        if (!naive && !front) scattered = false;  // the specification's opaque-inside rule
+      } else if (sc.kind[b] == RT_METAL) {  // material.h:42-64
+        const gvec ud = unnorm ? gunit(d) : d;
+        const float kk = -2.0f * gdot(ud, nrm);
+        const gvec refl = gfma(kk, nrm, ud);
+        const gvec u = unit_vector();
+        sd = gfma(sc.param[b], u, refl);
+        scattered = gdot(sd, nrm) > 0.0f && (naive || front);
+      } else {  // material.h:66-104
+        const float ratio = front ? sc.inv_param[b] : sc.param[b];
+        const gvec ud = unnorm ? gunit(d) : d;
+        const float cos_t = std::fmin(-gdot(ud, nrm), 1.0f);
+        const float sin_t = std::sqrt(fmaf_(-cos_t, cos_t, 1.0f));
+        const bool cannot = ratio * sin_t > 1.0f;
+        const float r0 = sc.r0[b];
+        const float refl = fmaf_(1.0f - r0, std::pow(1.0f - cos_t, 5.0f), r0);
+        if (cannot || refl > dr.next()) {
+          const float kk = -2.0f * gdot(ud, nrm);
+          sd = gfma(kk, nrm, ud);
+        } else {
+          const gvec qv = gmul(ratio, gfma(cos_t, nrm, ud));
+          const float m = -std::sqrt(std::fabs(1.0f - gdot(qv, qv)));
+          sd = gfma(m, nrm, qv);
+        }
+      }
+      if (!scattered) break;
+      att = gvec{att.x * sc.ar[b], att.y * sc.ag[b], att.z * sc.ab[b]};
+      o = p;
+      d = sd;
+      if (!unnorm) normalize3(d.x, d.y, d.z);
+    }
+    const float v[3] = {col3.x, col3.y, col3.z};
+    for (int j = 0; j < 3; ++j) {
+      fsum[j] += v[j];
+      const float x = v[j] * qscale;
+      q[j] += (uint32_t)x;
+    }
+  }
+  for (int a = 0; a < 3; ++a) acc[a] = (mode & GREF_FP32_SUM) ? fsum[a] : (float)q[a] * qinv;
+  return segs;
+}
+
 kscene make_kscene(const rt_scene_view &v) {
   kscene s;
   for (uint32_t i = 0; i < v.n; ++i) {
@@ -731,15 +993,18 @@ int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, co
       if (k >= 1) threads = std::min(threads, k);
     }
   }
-  std::atomic<int> next_row{0};
+  // work items of 64 pixels (a band of 8 rows still spreads over every thread)
+  const long long n_px = (long long)p->local_rows * p->width;
+  std::atomic<long long> next{0};
   std::atomic<unsigned long long> total{0};
   auto worker = [&]() {
     unsigned long long segs = 0;
-    for (int lr; (lr = next_row.fetch_add(1)) < p->local_rows;) {
-      const int band = lr / p->row_block;
-      const int grow = (band * p->band_stride + p->band_offset) * p->row_block + lr % p->row_block;
-      for (int col = 0; col < p->width; ++col) {
-        float *o = out + 3 * ((size_t)lr * p->width + col);
+    for (long long i0; (i0 = next.fetch_add(64)) < n_px;) {
+      for (long long i = i0; i < std::min(n_px, i0 + 64); ++i) {
+        const int lr = (int)(i / p->width), col = (int)(i % p->width);
+        const int band = lr / p->row_block;
+        const int grow = (band * p->band_stride + p->band_offset) * p->row_block + lr % p->row_block;
+        float *o = out + 3 * (size_t)i;
         if (grow >= p->height) {
           o[0] = o[1] = o[2] = 0.0f;
           continue;
@@ -760,6 +1025,42 @@ int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, co
 int rto_kernel_render(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
                       float *out, unsigned long long *segments, int threads) {
   return rto_kernel_render_exact(scene, cam, p, out, nullptr, 0, segments, threads);
+}
+
+int rto_gpuref_render(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p, int mode,
+                      float *out, unsigned long long *segments, int threads) {
+  if (!scene || !cam || !p || !out || p->width < 1 || p->height < 1 || p->row_block < 1 ||
+      p->band_stride < 1 || p->local_rows < 0 || p->spp < 0 || p->spp >= (1 << 24))
+    return -1;
+  const kscene sc = make_kscene(*scene);
+  kctx k{&sc, cam, p, (uint32_t)p->seed ^ ((uint32_t)(p->seed >> 32) * 0x9E3779B9u), true, true};
+  if (threads < 1) threads = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const long long n_px = (long long)p->local_rows * p->width;
+  std::atomic<long long> next{0};
+  std::atomic<unsigned long long> total{0};
+  auto worker = [&]() {
+    unsigned long long segs = 0;
+    for (long long i0; (i0 = next.fetch_add(64)) < n_px;) {
+      for (long long i = i0; i < std::min(n_px, i0 + 64); ++i) {
+        const int lr = (int)(i / p->width), col = (int)(i % p->width);
+        const int band = lr / p->row_block;
+        const int grow = (band * p->band_stride + p->band_offset) * p->row_block + lr % p->row_block;
+        float *o = out + 3 * (size_t)i;
+        if (grow >= p->height) {
+          o[0] = o[1] = o[2] = 0.0f;
+          continue;
+        }
+        segs += gpuref_pixel(k, col, grow, o, mode);
+      }
+    }
+    total += segs;
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < threads; ++t) pool.emplace_back(worker);
+  worker();
+  for (auto &t : pool) t.join();
+  if (segments) *segments = total.load();
+  return 0;
 }
 
 int rto_trace(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p, int col,

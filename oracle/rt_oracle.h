@@ -26,6 +26,11 @@ int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, co
                             float *out, double *exact, int no_dither, unsigned long long *segments,
                             int threads);
 /* fp64 final scene rows: kind, cx, cy, cz, r, albedo rgb, param (9 doubles). */
+/* src/gpu's own per-sample arithmetic with switches (mode: GREF_* bits in
+ * rt_oracle.cc), for attributing differences to the reference CUDA output;
+ * GPU semantics (open interval, metal fuzz with random_unit_vector). */
+int rto_gpuref_render(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p, int mode,
+                      float *out, unsigned long long *segments, int threads);
 /* debug: print one sample's segments and candidates to stdout */
 int rto_trace(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p, int col,
               int grow, long sample);
