@@ -329,6 +329,32 @@ def test_cli_reports_each_device_and_refuses_missing_gpus(rtow):
     assert bad.returncode == 2 and f"only {n} HIP device" in bad.stderr
 
 
+@pytest.mark.parametrize("kind,ends", [(0, True), (1, True), (2, False)])
+def test_opaque_sphere_hit_from_inside_ends_the_path(rtow, gpu_ctx, kind, ends, accel):
+    """a camera inside a lambertian or metal sphere of
+    radius 3 (the final scene around it) sees every primary ray hit that
+    sphere from inside, and the path ends there black: one segment per
+    sample, an all-zero image -- what the reference's path, trapped inside an
+    opaque sphere until the depth cap, returns.  Inside a glass sphere the
+    paths go on.  GPU == oracle bit for bit in every walk."""
+    import dataclasses
+    base = rtow.final_scene()
+    f32 = np.float32
+    big = dataclasses.replace(
+        base, cx=np.append(base.cx, f32(13)), cy=np.append(base.cy, f32(2)), cz=np.append(base.cz, f32(3)),
+        radius=np.append(base.radius, f32(3)), kind=np.append(base.kind, np.uint32(kind)),
+        albedo=np.vstack([base.albedo, np.array([[0.5, 0.6, 0.7]], f32)]),
+        param=np.append(base.param, f32(1.5 if kind == 2 else 0.3)))
+    cam = rtow.camera_cpu(aspect=2.0)  # eye (13, 2, 3): the new sphere's centre
+    p = rtow.make_params(32, 16, 4, seed=9)
+    got, st, want, segs = gpu_vs_oracle(rtow, gpu_ctx, big, cam, p, accel)
+    assert_bit_exact(got, st, want, segs)
+    if ends:
+        assert segs == 32 * 16 * 4 and not got.any()
+    else:
+        assert segs > 32 * 16 * 4 and got.any()
+
+
 def test_scene_upload_rejects_non_finite_centres(rtow, gpu_ctx):
     s = rtow.final_scene()
     cx = s.cx.copy()

@@ -149,11 +149,17 @@ def test_final_scene_gpu_semantics_vs_reference_gpu_gallery_image23(rtow, gpu_ct
     (src/gpu: 1920x1080, 500 spp, depth 50, defocus 0.6 at focus 10), re-rendered
     by the product with src/gpu's semantics from the same scene: the run's time
     seed is recovered (tests/gallery_lib.py) and its XORWOW draws restated.
-    Two seeds of ours give the noise floor.  Bounds: image-mean bias <= 0.25
-    level per channel (a quarter of north_star's 1/255) and 8x8 block error
-    <= 2x our seed-to-seed floor.  Measured: ours is 0.17-0.19 level brighter
-    (0.13-0.14 with the reference's own unrefined fp32 roots) and
-    the block error is 1.64x the floor (0.23 vs 0.14 level)."""
+    Two seeds of ours give the noise floor.  Ours is 0.17-0.19 level brighter
+    and the block error is 1.64x the floor (0.23 vs 0.14 level).  That
+    difference is explained (profiles/r03_image23_attribution.log,
+    tests/test_oracle.py::test_image23_brightness_is_src_gpu_fp32_hit_arithmetic):
+    the oracle's restatement of src/gpu's own fp32 hit arithmetic (its
+    quadratic on unnormalised directions, unrefined roots) renders the same
+    rows within 0.008 level of the gallery and 1.03x its floor, and the
+    specification is +0.169 / +0.176 / +0.200 level above that restatement,
+    i.e. +0.164 / +0.169 / +0.192 above the gallery.  Bounds: the bias within
+    0.03 level of that explained value per channel (seed noise ~0.003), block
+    error <= 1.75x our seed-to-seed floor."""
     from gallery_lib import src_gpu_final_scene
     from test_oracle import gallery_blocks
     gpu_ctx.upload(src_gpu_final_scene(rtow))
@@ -169,8 +175,9 @@ def test_final_scene_gpu_semantics_vs_reference_gpu_gallery_image23(rtow, gpu_ct
     err, floor = float(np.abs(a - g).mean()), float(np.abs(a - b).mean())
     report = {"bias": bias.round(4).tolist(), "block_err": round(err, 4), "block_floor": round(floor, 4)}
     print("image23", report)
-    assert np.all(np.abs(bias) <= 0.25), report
-    assert err <= 2.0 * floor, report
+    explained = np.array([0.164, 0.169, 0.192])
+    assert np.all(np.abs(bias - explained) <= 0.03), report
+    assert err <= 1.75 * floor, report
 
 
 # ------------------------------------------------------------ write_color --
