@@ -192,7 +192,7 @@ def gallery_compare(a, b, name="image22"):
     Bounds: 8x8 block-mean error <= 1.1 x our own seed-to-seed floor, and
     image-mean bias per channel <= max(4 sigma, 0.1 level).  The reference's
     image22 is ~0.05 level darker in red and green than ours (5 sigma at 2 M
-    pixels), partly from its unrefined fp32 roots (DESIGN.md 4, image23);
+    pixels), from its fp32 hit arithmetic (DESIGN.md 4, attributed on image23);
     0.1 level is a tenth of north_star's 1/255."""
     g = gallery_blocks(name)
     n = a.shape[0] * a.shape[1]
