@@ -104,3 +104,15 @@ def test_bench_two_ranks_gloo_traces_the_same_frames(tmp_path):
     assert two["value"] > 0 and one["first_frame_ms"] > 0
     a, b = (tmp_path / "one.ppm").read_bytes(), (tmp_path / "two.ppm").read_bytes()
     assert a.startswith(b"P3\n256 144\n255\n") and a == b
+    # the N > 1 line's extra fields: the step split into
+    # render / write_color / gather, no counter fields from another share's
+    # summary (this frame has none: nulls with a reason), cpu_baseline null
+    # with a note
+    parts = two["step_parts_ms"]
+    assert parts["render_max_over_ranks"] > 0 and parts["gather_max_over_ranks"] > 0
+    assert parts["render_max_over_ranks"] <= two["ms_per_step"]
+    roof = two["roofline"]
+    assert roof["valu_issue"] is None and roof["hbm"] is None and roof["pmc_null_reason"]
+    assert 0 < roof["frac"] <= 1
+    assert two["cpu_baseline"] is None and two["cpu_baseline_note"]
+    assert one["step_parts_ms"]["gather_max_over_ranks"] < 0.05  # no gather at N = 1
