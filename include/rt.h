@@ -269,6 +269,13 @@ int rt_render_async(rt_context *ctx, const rt_camera *cam, const rt_params *para
 int rt_render(rt_context *ctx, const rt_camera *cam, const rt_params *params,
               float *host_rgb, rt_stats *stats);
 
+/* Progress of the last rt_render_async / rt_render of this context, without
+ * blocking: how many of its bounded launches (RT_OPT_LAUNCH_SAMPLES) have
+ * completed, of how many.  RT_ERR_HIP if the device reported a fault in one
+ * of them -- the early failure report the reference's one launch cannot give
+ * (src/gpu/main.cu:130-131 learns of a fault only at cudaDeviceSynchronize). */
+int rt_render_progress(rt_context *ctx, uint32_t *launches_done, uint32_t *launches_total);
+
 /* Stats of the last rt_render_async (or, with RT_FLAG_KEEP_COUNTERS, of all
  * launches since rt_reset_stats); call after the stream has completed. */
 int rt_collect_stats(rt_context *ctx, rt_stats *stats);

@@ -277,6 +277,26 @@ int main(int argc, char **argv) {
     (void)hipSetDevice(devs[g]);
     (void)hipEventRecord(ev[4 * g + 3], streams[g]);
   }
+  // progress while the bounded launches run (the reference's "Scanlines
+  // remaining", src/cpu/main.cc:112): a render of many launches reports each
+  // one as it completes, and a device fault ends the run after the launch it
+  // happened in, not at the end of the frame
+  for (unsigned last = ~0u;;) {
+    unsigned done = 0, total = 0;
+    for (int g = 0; g < o.gpus; ++g) {
+      uint32_t d = 0, t = 0;
+      check(rt_render_progress(ctxs[g], &d, &t), "rt_render_progress");
+      done += d;
+      total += t;
+    }
+    if (!o.quiet && total > (unsigned)o.gpus && total - done != last) {
+      std::fprintf(stderr, "\rLaunches remaining: %u ", total - done);
+      std::fflush(stderr);
+      last = total - done;
+    }
+    if (done == total) break;
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  }
   for (int g = 0; g < o.gpus; ++g) {
     (void)hipSetDevice(devs[g]);
     if (hipStreamSynchronize(streams[g]) != hipSuccess) die("render", RT_ERR_HIP);

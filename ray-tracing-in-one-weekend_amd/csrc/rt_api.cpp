@@ -64,10 +64,10 @@ struct rt_context {
   hipEvent_t ev_done = nullptr;
   hipStream_t last_stream = nullptr;
   bool have_done = false;
-  // rt_render: one event after each bounded launch, waited on in turn (a
-  // fault surfaces after the launch it happened in)
+  // one event after each bounded launch of the last render: rt_render waits
+  // on them in turn (a fault surfaces after the launch it happened in),
+  // rt_render_progress queries them
   std::vector<hipEvent_t> ev_launch;
-  bool record_launches = false;
   double tonemap_thr64[257];  // rt_tonemap_async level thresholds (see tonemap_thresholds)
   float tonemap_thr32[257];
   double *d_thr64 = nullptr;
@@ -502,7 +502,7 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
   // zeroed frame (after the pilot, which renders into it too); finish_sums
   // converts them
   if (kp.sum_atomic) RT_HIP(hipMemsetAsync(accum_rgb, 0, frame_floats * sizeof(float), st));
-  if (c->record_launches) {
+  {
     while (c->ev_launch.size() < (size_t)chunks) {
       hipEvent_t ev = nullptr;
       RT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -516,7 +516,7 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
     kp.s_cnt = (int)(s1 - s0);
     // a launch that cannot start (bad configuration, lost device) stops the render here
     RT_HIP(rtk::launch_render(v, (unsigned)(blocks * units), lds, st, kp));
-    if (c->record_launches) RT_HIP(hipEventRecord(c->ev_launch[(size_t)k], st));
+    RT_HIP(hipEventRecord(c->ev_launch[(size_t)k], st));
   }
   c->last_launches += (uint32_t)chunks;
   c->enq_launches = (uint32_t)chunks;
@@ -538,8 +538,23 @@ int rt_render_async(rt_context *c, const rt_camera *cam, const rt_params *prm, f
   if (cam->model != RT_CAMERA_CPU && cam->model != RT_CAMERA_GPU) return RT_ERR_INVALID;
   if (cam->model == RT_CAMERA_CPU && (prm->width < 2 || prm->height < 2)) return RT_ERR_INVALID;
   if (!c->d_geom) return RT_ERR_NO_SCENE;
-  c->record_launches = false;
   return render_enqueue(c, cam, prm, accum_rgb, stream ? (hipStream_t)stream : c->stream, nullptr);
+}
+
+int rt_render_progress(rt_context *c, uint32_t *done, uint32_t *total) {
+  if (!c || !done || !total) return RT_ERR_INVALID;
+  const uint32_t n = std::min<uint32_t>(c->enq_launches, (uint32_t)c->ev_launch.size());
+  *total = n;
+  *done = 0;
+  RT_HIP(hipSetDevice(c->device));
+  // launches complete in order on their stream: count the leading finished ones
+  for (uint32_t k = 0; k < n; ++k) {
+    const hipError_t e = hipEventQuery(c->ev_launch[k]);
+    if (e == hipErrorNotReady) break;
+    if (e != hipSuccess) return hip_fail(e);  // a fault in or before launch k
+    ++*done;
+  }
+  return RT_OK;
 }
 
 int rt_reset_stats(rt_context *c, void *stream) {
@@ -588,10 +603,8 @@ int rt_render(rt_context *c, const rt_camera *cam, const rt_params *prm, float *
   if (cam->model == RT_CAMERA_CPU && (prm->width < 2 || prm->height < 2)) return RT_ERR_INVALID;
   if (!c->d_geom) return RT_ERR_NO_SCENE;
   // ev0 is recorded right before the render kernel (after a first-frame pilot)
-  c->record_launches = true;
   int st = render_enqueue(c, cam, prm, c->d_frame, c->stream, c->ev0);
   const uint32_t n_launch = std::min<uint32_t>(c->enq_launches, (uint32_t)c->ev_launch.size());
-  c->record_launches = false;
   if (st != RT_OK) return st;
   RT_HIP(hipEventRecord(c->ev1, c->stream));
   // wait launch by launch: a fault surfaces after the launch it happened in

@@ -128,6 +128,9 @@ def lib():
                                 ctypes.c_void_p, ctypes.POINTER(Stats)]
         L.rt_collect_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(Stats)]
         L.rt_reset_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        if hasattr(L, "rt_render_progress"):
+            L.rt_render_progress.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
+                                             ctypes.POINTER(ctypes.c_uint32)]
         L.rt_tonemap_u8.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
         L.rt_tonemap_u8_mode.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_void_p]
@@ -351,6 +354,12 @@ class Context:
         """write_color on the device: fp32 sums -> bytes, both device pointers."""
         check(lib().rt_tonemap_async(self._h, ctypes.c_void_p(dev_sums), n_pixels, spp, mode,
                                      ctypes.c_void_p(dev_out), ctypes.c_void_p(stream)), "rt_tonemap_async")
+
+    def progress(self):
+        """rt_render_progress: (launches done, launches total) of the last render."""
+        d, t = ctypes.c_uint32(), ctypes.c_uint32()
+        check(lib().rt_render_progress(self._h, ctypes.byref(d), ctypes.byref(t)), "rt_render_progress")
+        return d.value, t.value
 
     def reset_stats(self, stream=0):
         check(lib().rt_reset_stats(self._h, ctypes.c_void_p(stream)), "rt_reset_stats")

@@ -327,6 +327,33 @@ def test_cli_reports_each_device_and_refuses_missing_gpus(rtow):
     n = rtow.device_count()
     bad = subprocess.run(args + ["--gpus", str(n + 1)], capture_output=True, timeout=120, text=True)
     assert bad.returncode == 2 and f"only {n} HIP device" in bad.stderr
+    # a render long enough for several bounded launches reports its progress
+    big = [exe, "--width", "1920", "--height", "1080", "--spp", "2100", "--seed", "5", "--out", os.devnull]
+    r = subprocess.run(big, capture_output=True, timeout=120, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Launches remaining: 0" in r.stderr and re.search(r"render [0-9.]+ ms in 2 launch", r.stderr), r.stderr
+
+
+def test_render_progress_counts_bounded_launches(rtow, gpu_ctx):
+    """rt_render_progress after an asynchronous render of 5 bounded launches:
+    (5, 5) once the stream has drained, and the image equals one launch's."""
+    import torch
+    gpu_ctx.upload(rtow.final_scene())
+    cam = rtow.camera_cpu(aspect=320 / 180)
+    p = rtow.make_params(320, 180, 50, seed=4, flags=1 << 9, units=1)
+    want, _ = gpu_ctx.render(cam, p)
+    assert gpu_ctx.progress() == (1, 1)
+    gpu_ctx.set_option(rtow.RT_OPT_LAUNCH_SAMPLES, 320 * 180 * 10)
+    dev = torch.device("cuda", 0)
+    t = torch.zeros((180, 320, 3), dtype=torch.float32, device=dev)
+    st = torch.cuda.Stream(dev)
+    gpu_ctx.render_async(cam, p, t.data_ptr(), st.cuda_stream)
+    done, total = gpu_ctx.progress()
+    assert total == 5 and 0 <= done <= 5
+    torch.cuda.synchronize(dev)
+    assert gpu_ctx.progress() == (5, 5)
+    assert np.array_equal(t.cpu().numpy(), want)
+    gpu_ctx.set_option(rtow.RT_OPT_LAUNCH_SAMPLES, 0)
 
 
 @pytest.mark.parametrize("kind,ends", [(0, True), (1, True), (2, False)])
