@@ -229,7 +229,9 @@ typedef enum {
   RT_OPT_BVH_SIDE = 5,        /* SAH weight of the x- and z-facing sides (default 1) */
   /* at most this many samples (pixels x samples per pixel) per render kernel
    * launch (default 2^32): a render is split into sample-range launches that
-   * each stay well under a second (no monolithic launch) */
+   * each stay well under a second (no monolithic launch).  A launch
+   * always covers every pixel of the tile with at least one sample, so a
+   * budget below the pixel count gives spp launches of one sample each. */
   RT_OPT_LAUNCH_SAMPLES = 6
 } rt_option;
 enum { RT_GRID_AUTO = 0, RT_GRID_LDS = 1, RT_GRID_CELLS_LDS = 2, RT_GRID_GLOBAL = 3 };

@@ -327,7 +327,9 @@ class Context:
 
     def upload(self, scene, grid_mode=None, grid_scale=None):
         """rt_scene_upload; grid_mode ("auto", "lds", "cells", "global") and
-        grid_scale set the layer grid's options first (the image is the same)."""
+        grid_scale set the layer grid's options first (the image is the same).
+        Options are the context's: they stay set for later uploads until set
+        again (0 / "auto" restores the default)."""
         if grid_mode is not None:
             self.set_option(RT_OPT_GRID_PLACEMENT, GRID_PLACEMENTS[grid_mode])
         if grid_scale is not None:
