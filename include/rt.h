@@ -169,7 +169,7 @@ typedef struct {
   double kernel_ms;      /* hipEvent time of the render kernel (0 if async) */
   uint64_t root_tests;   /* RT_FLAG_COUNT_WORK: per alive lane and bounce, the spheres whose
                             root / interval code the wave executed (some lane's line met it) */
-  uint64_t launches;     /* render kernel launches (bounded sample ranges, RT_OPT_LAUNCH_SAMPLES) */
+  uint64_t launches;     /* render kernel launches (bounded block / sample ranges, RT_OPT_LAUNCH_SAMPLES) */
 } rt_stats;
 
 typedef struct rt_context rt_context;
@@ -227,11 +227,14 @@ typedef enum {
   RT_OPT_BVH_LEAF = 3,        /* spheres per BVH leaf, 1..4 (default 4) */
   RT_OPT_BVH_COLLAPSE = 4,    /* BVH node collapse area ratio (default 0.35) */
   RT_OPT_BVH_SIDE = 5,        /* SAH weight of the x- and z-facing sides (default 1) */
-  /* at most this many samples (pixels x samples per pixel) per render kernel
-   * launch (default 2^32): a render is split into sample-range launches that
-   * each stay well under a second (no monolithic launch).  A launch
-   * always covers every pixel of the tile with at least one sample, so a
-   * budget below the pixel count gives spp launches of one sample each. */
+  /* about this many samples (pixels x samples per pixel) per render kernel
+   * launch at most (default 2^32): a render is split into launches that each
+   * stay well under a second (no monolithic launch).  A launch
+   * runs a range of whole 4-tile blocks (at least 8192 of them, or the whole
+   * frame) with all of their samples; only when such a range is still over
+   * the budget are its samples split into sample ranges as well (a launch
+   * then holds at least one sample per pixel).  At most 65536 launches per
+   * render: a smaller budget is raised to total samples / 65536. */
   RT_OPT_LAUNCH_SAMPLES = 6
 } rt_option;
 enum { RT_GRID_AUTO = 0, RT_GRID_LDS = 1, RT_GRID_CELLS_LDS = 2, RT_GRID_GLOBAL = 3 };
@@ -251,8 +254,9 @@ int rt_scene_upload(rt_context *ctx, const rt_scene_view *scene);
  * own stream) writing params->width * params->local_rows * 3 floats to the
  * DEVICE pointer accum_rgb.  Replaces render<<<>>> (src/gpu/camera.h:169-195),
  * one monolithic launch in the reference (src/gpu/main.cu:130): here the
- * samples are split into launches of at most RT_OPT_LAUNCH_SAMPLES samples,
- * each checked for a launch error as it is enqueued.
+ * frame is split into launches of about RT_OPT_LAUNCH_SAMPLES samples at
+ * most (block ranges, then sample ranges), each checked for a launch error
+ * as it is enqueued.
  * Does not synchronise, also not on the first render of a frame geometry
  * with RT_FLAG_PILOT_SCHEDULE (the pilot and its sort are enqueued too).
  * Renders of one context on different streams run one after another (each
@@ -342,6 +346,15 @@ int rt_device_kat(int device, int kind, const double *in, size_t n_cases, double
 #define RT_ACCEL_INFO_N 18
 int rt_internal_accel_info(const rt_scene_view *scene, int grid_placement, double grid_scale, uint64_t *out,
                            size_t n_out);
+
+/* Host only (no device): how rt_render would cut a render with these
+ * parameters into launches under a launch-sample budget (0 = the default,
+ * 2^32; see RT_OPT_LAUNCH_SAMPLES).  Writes min(n_out, RT_LAUNCH_PLAN_N)
+ * values: 0 block ranges, 1 sample ranges per block range, 2 units (waves per
+ * tile), 3 work entries (blocks x units), 4 launches (ranges x sample ranges).
+ * For tests. */
+#define RT_LAUNCH_PLAN_N 5
+int rt_internal_launch_plan(const rt_params *params, double launch_samples, uint64_t *out, size_t n_out);
 
 #ifdef __cplusplus
 }

@@ -1,6 +1,6 @@
 // rt_api.cpp -- the host half of the C ABI (include/rt.h): device contexts,
 // scene upload, the render launches (pilot schedule, unit shares, bounded
-// sample-range launches), stats, the device tonemap and the diagnostics.
+// block- and sample-range launches), stats, the device tonemap and the diagnostics.
 // Host C++ over the HIP runtime; the kernels and their launch wrappers live
 // in rt_kernel.hip, the acceleration-structure builder in rt_accel.cpp.
 //
@@ -330,6 +330,72 @@ uint64_t valid_rows(const rt_params *prm) {
 // rt_render_async's body.  ev_start (may be null) is recorded on the stream
 // just before the render kernel itself, after any one-time setup (the pilot,
 // buffer growth), so that rt_render's kernel_ms times the render alone.
+// How a render is cut into launches (render_enqueue; rt_internal_launch_plan
+// shows it on the host).
+struct launch_plan {
+  long long units, ranges, chunks, entries;
+};
+launch_plan plan_launches(const rt_params *prm, double launch_samples) {
+  const long long tiles_x = (prm->width + rtk::kTile - 1) / rtk::kTile;
+  const long long tiles = tiles_x * ((prm->local_rows + rtk::kTile - 1) / rtk::kTile);
+  const long long blocks = (tiles + rtk::kWavesPerBlock - 1) / rtk::kWavesPerBlock;
+  const bool traced = prm->spp > 0 && prm->max_depth > 0;
+  const double frame_px = (double)prm->width * (double)prm->local_rows;
+  const double total = traced ? frame_px * prm->spp : 0.0;
+  const double budget = std::max(launch_samples, total / (double)rtk::kMaxLaunches);
+  // How many waves share a tile's samples (even shares; the integer pixel
+  // sums make any split give the same image).  One wave per tile traces all
+  // of its tile's samples; when a rank holds few tiles (a 1/8 share of a 4K
+  // frame is ~2 waves per wave slot), the slowest tiles (long glass / metal
+  // paths) then set the frame time, so the samples are split over `units`
+  // waves (tools/rank_times.py).
+  long long units = prm->units;
+  if (units <= 0) {
+    const bool pilot = (prm->flags & RT_FLAG_PILOT_SCHEDULE) != 0;
+    units = pilot ? std::llround((double)rtk::kPilotTilesPerUnit / (double)std::max(1LL, tiles))
+                  : (tiles < rtk::kSplitTiles ? rtk::kUnits : 1);
+    units = std::min<long long>(std::max(units, 1LL), rtk::kUnits);
+  }
+  if (!traced) units = 1;  // nothing is traced
+  units = std::max(1LL, std::min<long long>(units, prm->spp));  // >= 1 sample per unit
+  // Bounded launches: about `budget` samples per launch at most.
+  // The plain split is by samples: `chunks` launches over every work entry
+  // (a block of 4 tiles and a unit's share of their samples), each tracing
+  // spp / chunks samples per pixel.  That keeps the launches wide (their
+  // tails short) but shortens each wave's sample pool, whose own tail idles
+  // lanes: ~2.2 / s of them at s samples per pixel per wave (lane efficiency
+  // 0.995 at 500, 0.981 at 125, 0.861 at 16: C4's full frame on one GPU,
+  // profiles/r03n_bench_c4.log).  Below kMinPoolSpp the work entries are
+  // split too, into `ranges` strided subsets (range r runs entries r, r +
+  // ranges, ... of block_order, so every launch keeps the expensive-first
+  // order over a mix of the frame), and the samples into fewer, longer
+  // chunks of about kPoolSpp per wave.  (Contiguous entry ranges lost 6 % on
+  // C3's full frame to their launch tails,
+  // profiles/r03o_contiguous_ranges_bench_c3.log.)  The
+  // integer pixel sums make every split give the same image.
+  long long entries = (long long)blocks * units;
+  long long ranges = 1, chunks = 1;
+  if (total > budget) {
+    chunks = std::min<long long>(prm->spp, (long long)std::ceil(total / budget));
+    const long long u1 = std::max(1LL, std::min<long long>(units, prm->spp / chunks));
+    if ((double)prm->spp / (double)(u1 * chunks) >= rtk::kMinPoolSpp) {
+      units = u1;
+    } else {
+      chunks = std::max(1LL, (long long)std::floor((double)prm->spp / ((double)units * rtk::kPoolSpp)));
+      units = std::max(1LL, std::min<long long>(units, prm->spp / chunks));
+      entries = (long long)blocks * units;
+      ranges = std::min<long long>(entries, (long long)std::ceil(total / ((double)chunks * budget)));
+      // entries too few for the budget: more sample ranges
+      if (total / ((double)ranges * (double)chunks) > budget)
+        chunks = std::min<long long>(prm->spp, (long long)std::ceil(total / ((double)ranges * budget)));
+      units = std::max(1LL, std::min<long long>(units, prm->spp / chunks));
+      entries = (long long)blocks * units;
+      ranges = std::max(1LL, std::min({ranges, entries, rtk::kMaxLaunches / chunks}));
+    }
+  }
+  return launch_plan{units, ranges, chunks, entries};
+}
+
 int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, float *accum_rgb, hipStream_t st,
                    hipEvent_t ev_start) {
   RT_HIP(hipSetDevice(c->device));
@@ -353,6 +419,7 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
 
   rtk::kparams kp;
   std::memset(&kp, 0, sizeof kp);
+  kp.block_stride = 1;  // entry = blockIdx.x (the pilot; the launches below set their ranges)
   kp.cam = *cam;
   kp.width = prm->width;
   kp.height = prm->height;
@@ -419,27 +486,9 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
                 (grid ? rtk::kVarGrid : 0) | (place << rtk::kVarPlaceShift);
   const size_t lds = rtk::grid_lds_bytes(place, kp.grid_n_items, kp.grid_n_cells);
   const bool traced = prm->spp > 0 && prm->max_depth > 0;
-  // Bounded launches: the samples are split into `chunks` ranges
-  // of at most launch_samples samples of the tile each, one launch per range.
-  // The integer pixel sums make every split give the same image.
-  const double frame_px = (double)prm->width * (double)prm->local_rows;
-  long long chunks = traced ? (long long)std::ceil(frame_px * prm->spp / c->launch_samples) : 1;
-  chunks = std::max(1LL, std::min<long long>(chunks, prm->spp > 0 ? prm->spp : 1));
-  // How many waves share a tile's samples (even shares; the integer pixel
-  // sums make any split give the same image).  One wave per tile traces all
-  // of its tile's samples; when a rank holds few tiles (a 1/8 share of a 4K
-  // frame is ~2 waves per wave slot), the slowest tiles (long glass / metal
-  // paths) then set the frame time, so the samples are split over `units`
-  // waves (tools/rank_times.py).
-  long long units = prm->units;
-  if (units <= 0) {
-    const bool pilot = (prm->flags & RT_FLAG_PILOT_SCHEDULE) != 0;
-    units = pilot ? std::llround((double)rtk::kPilotTilesPerUnit / (double)std::max(1LL, tiles))
-                  : (tiles < rtk::kSplitTiles ? rtk::kUnits : 1);
-    units = std::min<long long>(std::max(units, 1LL), rtk::kUnits);
-  }
-  if (!traced) units = 1;  // nothing is traced
-  units = std::max(1LL, std::min<long long>(units, prm->spp / chunks));  // >= 1 sample per unit
+  const launch_plan lp = plan_launches(prm, c->launch_samples);
+  const long long units = lp.units, ranges = lp.ranges, chunks = lp.chunks, entries = lp.entries;
+  const long long launches = ranges * chunks;
   kp.units = (int)units;
   const int f = sum_bits(prm->spp);
   kp.qscale = std::ldexp(1.0f, f);
@@ -448,6 +497,7 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
   // sample (0.03 level at F = 20); stochastic rounding is unbiased for every
   // spp
   kp.dither = f < 20 ? 1 : 0;
+  // disjoint block ranges write disjoint pixels: float stores suffice
   kp.sum_atomic = (units > 1 || chunks > 1) ? 1 : 0;
   const uint64_t frame_floats = (uint64_t)prm->local_rows * (uint64_t)prm->width * 3u;
   if ((prm->flags & RT_FLAG_PILOT_SCHEDULE) && traced && blocks > 1) {
@@ -503,23 +553,31 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
   // converts them
   if (kp.sum_atomic) RT_HIP(hipMemsetAsync(accum_rgb, 0, frame_floats * sizeof(float), st));
   {
-    while (c->ev_launch.size() < (size_t)chunks) {
+    while (c->ev_launch.size() < (size_t)launches) {
       hipEvent_t ev = nullptr;
       RT_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
       c->ev_launch.push_back(ev);
     }
   }
   if (ev_start) RT_HIP(hipEventRecord(ev_start, st));
-  for (long long k = 0; k < chunks; ++k) {
-    const long long s0 = k * prm->spp / chunks, s1 = (k + 1) * prm->spp / chunks;
-    kp.s_lo = (int)s0;
-    kp.s_cnt = (int)(s1 - s0);
-    // a launch that cannot start (bad configuration, lost device) stops the render here
-    RT_HIP(rtk::launch_render(v, (unsigned)(blocks * units), lds, st, kp));
-    RT_HIP(hipEventRecord(c->ev_launch[(size_t)k], st));
+  long long k = 0;
+  kp.block_stride = (int)ranges;
+  for (long long r = 0; r < ranges; ++r) {
+    // entries r, r + ranges, r + 2 ranges, ... in block_order's order (most
+    // expensive first with the pilot)
+    kp.block_base = (int)r;
+    const long long n_r = (entries - r + ranges - 1) / ranges;
+    for (long long ch = 0; ch < chunks; ++ch, ++k) {
+      const long long s0 = ch * prm->spp / chunks, s1 = (ch + 1) * prm->spp / chunks;
+      kp.s_lo = (int)s0;
+      kp.s_cnt = (int)(s1 - s0);
+      // a launch that cannot start (bad configuration, lost device) stops the render here
+      RT_HIP(rtk::launch_render(v, (unsigned)n_r, lds, st, kp));
+      RT_HIP(hipEventRecord(c->ev_launch[(size_t)k], st));
+    }
   }
-  c->last_launches += (uint32_t)chunks;
-  c->enq_launches = (uint32_t)chunks;
+  c->last_launches += (uint32_t)launches;
+  c->enq_launches = (uint32_t)launches;
   if (kp.sum_atomic) RT_HIP(rtk::launch_finish_sums(reinterpret_cast<uint32_t *>(accum_rgb), frame_floats, kp.qinv, st));
   RT_HIP(hipEventRecord(c->ev_done, st));
   c->last_stream = st;
@@ -618,6 +676,17 @@ int rt_render(rt_context *c, const rt_camera *cam, const rt_params *prm, float *
     if (st != RT_OK) return st;
     stats->kernel_ms = ms;
   }
+  return RT_OK;
+}
+
+// Host-only view of how rt_render would cut a render into launches (no
+// device needed): tests/test_host.py checks the plans of the BASELINE configs.
+int rt_internal_launch_plan(const rt_params *prm, double launch_samples, uint64_t *out, size_t n_out) {
+  if (!out || !params_ok(prm) || !(launch_samples >= 0.0)) return RT_ERR_INVALID;
+  const launch_plan lp = plan_launches(prm, launch_samples > 0.0 ? launch_samples : rtk::kLaunchSamples);
+  const uint64_t v[RT_LAUNCH_PLAN_N] = {(uint64_t)lp.ranges, (uint64_t)lp.chunks, (uint64_t)lp.units,
+                                        (uint64_t)lp.entries, (uint64_t)(lp.ranges * lp.chunks)};
+  for (size_t i = 0; i < n_out && i < RT_LAUNCH_PLAN_N; ++i) out[i] = v[i];
   return RT_OK;
 }
 

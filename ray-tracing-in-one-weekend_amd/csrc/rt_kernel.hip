@@ -789,7 +789,8 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   // the lane its current pixel slot, sample and global pixel index; column and
   // row are recomputed where they are used.
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x) >> 6;
-  const unsigned bid = p.block_order ? as_const(p.block_order)[blockIdx.x] : blockIdx.x;
+  const unsigned entry = blockIdx.x * (unsigned)p.block_stride + (unsigned)p.block_base;
+  const unsigned bid = p.block_order ? as_const(p.block_order)[entry] : entry;
   const int unit = (int)(bid % (unsigned)p.units);
   const int tile = (int)(bid / (unsigned)p.units) * kWavesPerBlock + wave;
   const int col0 = (tile % p.tiles_x) * kTile, lrow0 = (tile / p.tiles_x) * kTile;

@@ -48,10 +48,17 @@ constexpr int kUnits = 8;  // without the pilot
 // profiles/r02zl_ab_counter_slots.log)
 constexpr int kCounterSlots = 32;
 // Bounded launches (failure detection): a render is split into
-// sample-range launches of at most this many samples (RT_OPT_LAUNCH_SAMPLES
+// launches of about this many samples at most (RT_OPT_LAUNCH_SAMPLES
 // overrides).  2^32 keeps the headline frame (4.15e9 samples, ~0.13 s) and a
-// C3 rank share in one launch and cuts a C4 rank share (6.7e10) into 16.
+// C3 rank share in one launch and cuts a C4 rank share (6.7e10) into 16
+// sample ranges of 125 spp.  When sample ranges alone would leave fewer than
+// kMinPoolSpp samples per pixel per wave, the work entries are split into
+// strided ranges as well and the samples into chunks of ~kPoolSpp
+// (rt_api.cpp plan_launches).  At most kMaxLaunches launches per render.
 constexpr double kLaunchSamples = 4294967296.0;
+constexpr double kMinPoolSpp = 100.0;
+constexpr double kPoolSpp = 250.0;
+constexpr long long kMaxLaunches = 65536;
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef float f4 __attribute__((ext_vector_type(4)));
@@ -116,6 +123,8 @@ struct kparams {
   // `units` waves per tile: block b traces samples [s_lo + u s_cnt / units,
   // s_lo + (u + 1) s_cnt / units), u = b % units
   int units, s_lo, s_cnt;
+  // this launch's work entries: blockIdx.x * block_stride + block_base
+  // indexes block_order (or is the entry itself), entries [0, blocks * units)
   // 0: the wave stores its tile's pixels as floats (one launch, one unit);
   // 1: it adds its integer sums into the frame with atomics (several units or
   // launches per tile; finish_sums converts at the end)
@@ -125,7 +134,8 @@ struct kparams {
   // spp); q truncates, or, when dither != 0 (F < 20: spp >= 4096), rounds
   // stochastically (unbiased for every spp)
   float qscale, qinv;  // 2^F, 2^-F
-  int dither, pad_d;
+  int dither, block_base;
+  int block_stride, pad_b;
   // device buffers (rt_context; out = the caller's frame tile)
   const struct pair_geom *scan_geom;  // brute-force order
   const struct pair_geom *geom;       // BVH leaf order

@@ -142,6 +142,9 @@ def lib():
                                    ctypes.c_int]
         L.rt_internal_accel_info.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double,
                                              ctypes.c_void_p, ctypes.c_size_t]
+        if hasattr(L, "rt_internal_launch_plan"):
+            L.rt_internal_launch_plan.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p,
+                                                  ctypes.c_size_t]
         if hasattr(L, "rt_context_set_option"):  # (absent in pre-ABI-4 builds loaded for A/B runs)
             L.rt_context_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
         _lib = L
@@ -408,6 +411,19 @@ def accel_info(scene, grid_mode="auto", grid_scale=0.0):
     check(lib().rt_internal_accel_info(ctypes.byref(v), GRID_PLACEMENTS[grid_mode], float(grid_scale),
                                        out.ctypes.data, out.size), "rt_internal_accel_info")
     return {k: int(x) for k, x in zip(ACCEL_INFO_KEYS, out)}
+
+
+LAUNCH_PLAN_KEYS = ("ranges", "chunks", "units", "entries", "launches")
+
+
+def launch_plan(params, launch_samples=0.0):
+    """How rt_render would cut a render with `params` into launches under a
+    launch-sample budget (0 = default), computed on the host
+    (rt_internal_launch_plan; no device): a dict of LAUNCH_PLAN_KEYS."""
+    out = np.zeros(len(LAUNCH_PLAN_KEYS), np.uint64)
+    check(lib().rt_internal_launch_plan(ctypes.byref(params), float(launch_samples), out.ctypes.data, out.size),
+          "rt_internal_launch_plan")
+    return {k: int(x) for k, x in zip(LAUNCH_PLAN_KEYS, out)}
 
 
 def write_ppm(path, rgb, binary=False):

@@ -329,20 +329,23 @@ def test_stochastic_rounding_bit_exact_vs_oracle(rtow, gpu_ctx, oracle):
 
 
 def test_bounded_launches_give_the_same_image(rtow, gpu_ctx):
-    """a render is split into sample-range launches of at most
-    RT_OPT_LAUNCH_SAMPLES samples.  C4's rank-0 share (2048 x 16384 pixels,
-    10 000 spheres) at 16 spp with a budget of 2^26 samples runs as 8
-    launches; its image and segments equal the one-launch render bit for bit,
-    and so do 3 launches with 2 units per tile.  At the default budget
+    """a render is split into launches of about
+    RT_OPT_LAUNCH_SAMPLES samples at most.  C4's rank-0 share (2048 x 16384
+    pixels, 10 000 spheres) at 16 spp (too few samples to split) with a
+    budget of 2^26 samples runs as 8 strided entry-range launches with all 16
+    samples each (float stores, no atomics); with 2 units per tile and a
+    2.0e8 budget as 3; with a 2^24 budget as 32.  Every image and segment
+    count equals the one-launch render bit for bit.  At the default budget
     (2^32) the headline frame (3840x2160x500 = 4.15e9 samples) stays one
-    launch, and C4's full share at 2000 spp (6.7e10) would be 16."""
+    launch, and C4's full share at 2000 spp (6.7e10) is 16 sample ranges
+    (test_host.py test_launch_plan)."""
     scene = rtow.final_scene(half_extent=50)
     gpu_ctx.upload(scene)
     cam = rtow.camera_cpu(aspect=1.0)
     p = band_params(rtow, 16384, 16384, 16, 8, 0, seed=420, flags=GRID, units=1)
     one, s1 = gpu_ctx.render(cam, p)
     assert s1.launches == 1
-    for budget, units, launches in ((1 << 26, 1, 8), (2048 * 16384 * 6, 2, 3)):
+    for budget, units, launches in ((1 << 26, 1, 8), (2048 * 16384 * 6, 2, 3), (1 << 24, 1, 32)):
         gpu_ctx.set_option(rtow.RT_OPT_LAUNCH_SAMPLES, budget)
         p.units = units
         img, st = gpu_ctx.render(cam, p)

@@ -167,7 +167,7 @@ def test_ppm_writer_p3_and_p6(rtow, tmp_path):
 def test_abi_exports_every_declared_symbol(rtow):
     hdr = open(os.path.join(ROOT, "include", "rt.h")).read()
     names = sorted(set(re.findall(r"^\s*(?:[\w\*\s]+?)\b(rt_\w+)\s*\(", hdr, re.M)))
-    assert len(names) == 23, names
+    assert len(names) == 24, names
     L = rtow.lib()
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
@@ -175,6 +175,44 @@ def test_abi_exports_every_declared_symbol(rtow):
                          text=True, check=True).stdout
     for n in names:
         assert re.search(rf"\bT {n}$", out, re.M), n
+
+
+@pytest.mark.parametrize("w,h,spp,world,budget,plan", [
+    # headline frame (4.15e9 samples) and C1: one launch
+    (3840, 2160, 500, 1, 0, (1, 1, 1, 32400)),
+    (1920, 1080, 100, 1, 0, (1, 1, 4, 32400)),
+    # C3 and C4 rank shares (1/8): C3 one launch, C4 16 sample ranges of 125 spp
+    (7680, 4320, 1000, 8, 0, (1, 1, 2, 32640)),
+    (16384, 16384, 2000, 8, 0, (1, 16, 1, 131072)),
+    # whole C3 frame on one GPU: 8 sample ranges of 125 spp
+    (7680, 4320, 1000, 1, 0, (1, 8, 1, 129600)),
+    # whole C4 frame on one GPU: sample ranges alone would leave 16 spp per
+    # wave; 16 strided entry ranges x 8 sample ranges of 250 spp instead
+    (16384, 16384, 2000, 1, 0, (16, 8, 1, 1048576)),
+    # the CLI's progress test: 1080p at 2100 spp, 2 sample ranges of 1050 spp
+    (1920, 1080, 2100, 1, 0, (1, 2, 4, 32400)),
+    # a small frame at 50 spp over the budget: 5 entry ranges, all 50 samples each
+    (320, 180, 50, 1, 320 * 180 * 10, (5, 1, 1, 230)),
+    # C4's share at 16 spp and a 2^24 budget: 32 entry ranges
+    (16384, 16384, 16, 8, 1 << 24, (32, 1, 1, 131072)),
+    # a budget below total / 65536 is raised: at most 65536 launches
+    (16384, 16384, 2000, 1, 1, (8192, 8, 1, 1048576)),
+])
+def test_launch_plan(rtow, w, h, spp, world, budget, plan):
+    """rt_internal_launch_plan: how rt_render cuts a render into bounded
+    launches (include/rt.h RT_OPT_LAUNCH_SAMPLES): sample ranges over every
+    work entry while each wave keeps >= 100 samples per pixel; else strided
+    entry ranges x sample ranges of ~250 spp (a short sample pool idles lanes
+    at its tail: C4's full frame in 16-spp sample ranges ran at lane
+    efficiency 0.861, profiles/r03n_bench_c4.log)."""
+    flags = rtow.RT_FLAG_ACCEL_BVH | rtow.RT_FLAG_PILOT_SCHEDULE
+    units = 1 if budget == 320 * 180 * 10 else 0
+    got = rtow.launch_plan(rtow.make_params(w, h, spp, flags=flags, world=world, units=units), budget)
+    assert (got["ranges"], got["chunks"], got["units"], got["entries"]) == plan, got
+    assert got["launches"] == got["ranges"] * got["chunks"] <= 65536
+    samples = w * h * spp / world
+    if got["launches"] > 1:  # each launch within the budget (up to padding pixels)
+        assert samples / got["launches"] <= max(budget or 2 ** 32, samples / 65536) * 1.01
 
 
 def test_invalid_arguments_return_status(rtow):
