@@ -6,6 +6,7 @@
 // abort on their own findings).
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <fcntl.h>
 #include <unistd.h>
@@ -107,6 +108,28 @@ int main() {
     CHECK(rt_write_ppm(fd, rgb.data(), w, h, 0) == RT_OK);
     CHECK(rt_write_ppm(fd, rgb.data(), w, h, 1) == RT_OK);
     close(fd);
+  }
+  // launch plans (rt_internal_launch_plan): frames from one pixel to C4's,
+  // spp up to the ABI's maximum, budgets from 1 sample to 2^40
+  for (int w : {1, 9, 3840, 16384}) {
+    for (int spp : {0, 1, 16, 2000, (1 << 24) - 1}) {
+      for (double budget : {0.0, 1.0, 1e6, 4294967296.0, 1099511627776.0}) {
+        rt_params p;
+        std::memset(&p, 0, sizeof p);
+        p.width = w;
+        p.height = w;
+        p.spp = spp;
+        p.max_depth = 50;
+        p.row_block = w;
+        p.band_stride = 1;
+        p.local_rows = w;
+        p.flags = RT_FLAG_ACCEL_BVH | RT_FLAG_PILOT_SCHEDULE;
+        uint64_t plan[RT_LAUNCH_PLAN_N];
+        CHECK(rt_internal_launch_plan(&p, budget, plan, RT_LAUNCH_PLAN_N) == RT_OK);
+        CHECK(plan[0] >= 1 && plan[1] >= 1 && plan[2] >= 1 && plan[4] == plan[0] * plan[1] && plan[4] <= 65536);
+        CHECK(plan[0] <= plan[3] && (spp == 0 || plan[1] <= (uint64_t)spp));
+      }
+    }
   }
   std::printf("host_sanitize: ok\n");
   return 0;
