@@ -247,7 +247,9 @@ int rt_context_set_option(rt_context *ctx, int option, double value);
  * and the albedos of lambertian and metal spheres in [0, 1] (RT_ERR_INVALID
  * otherwise: the fixed-point pixel sums need a sample's radiance <= 1 -- a
  * deliberate narrowing of the reference, which renders energy-creating
- * albedos too; every scene of the reference is inside it). */
+ * albedos too; every scene of the reference is inside it).  Metal fuzz above
+ * 1 is clamped to 1, as the reference's metal constructors do
+ * (src/cpu/material.h:38, src/gpu/material.h:45). */
 int rt_scene_upload(rt_context *ctx, const rt_scene_view *scene);
 
 /* Enqueue the render kernel on `stream` (a hipStream_t, NULL = the context's

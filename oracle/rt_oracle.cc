@@ -901,7 +901,8 @@ kscene make_kscene(const rt_scene_view &v) {
     s.ar.push_back(v.albedo_rgb[3 * i + 0]);
     s.ag.push_back(v.albedo_rgb[3 * i + 1]);
     s.ab.push_back(v.albedo_rgb[3 * i + 2]);
-    s.param.push_back(v.mat_param[i]);
+    // metal fuzz clamped to 1 (material.h:38), as rt_scene_upload does
+    s.param.push_back(v.mat_kind[i] == RT_METAL ? std::min(v.mat_param[i], 1.0f) : v.mat_param[i]);
     const double ior = v.mat_param[i];
     s.inv_param.push_back((float)(1.0 / ior));
     const double r0 = (1.0 - ior) / (1.0 + ior);
@@ -914,6 +915,14 @@ kscene make_kscene(const rt_scene_view &v) {
 }  // namespace
 
 extern "C" {
+
+namespace {
+// main.cc:78-130 from the camera on, for a world already built (and the rng
+// at the state the scene left it in)
+int reference_render_world(dworld &w, rng64 &r, d3 lookfrom, d3 lookat, double aperture, double focus,
+                           int width, double aspect, int spp, int max_depth, uint8_t *rgb_out,
+                           unsigned long long *segments);
+}  // namespace
 
 int rto_reference_render(int width, double aspect, int spp, int max_depth, int scene,
                          uint8_t *rgb_out, int *height_out, unsigned long long *segments) {
@@ -935,6 +944,36 @@ int rto_reference_render(int width, double aspect, int spp, int max_depth, int s
   } else {
     final_scene(r, 11, w.s);
   }
+  return reference_render_world(w, r, lookfrom, lookat, aperture, focus, width, aspect, spp, max_depth,
+                                rgb_out, segments);
+}
+
+int rto_reference_render_view(const rt_scene_view *scene, int width, double aspect, int spp, int max_depth,
+                              uint8_t *rgb_out, int *height_out, unsigned long long *segments) {
+  if (!scene || width < 2 || !(aspect > 0) || spp < 1 || max_depth < 0) return -1;
+  const int height = (int)(width / aspect);
+  if (height < 2) return -1;
+  if (height_out) *height_out = height;
+  if (!rgb_out) return 0;
+  rng64 r;  // no scene draws: the stream starts at the first sample
+  dworld w;
+  for (uint32_t i = 0; i < scene->n; ++i) {
+    const uint32_t k = scene->mat_kind[i];
+    const double p = scene->mat_param[i];
+    const d3 alb{scene->albedo_rgb[3 * i], scene->albedo_rgb[3 * i + 1], scene->albedo_rgb[3 * i + 2]};
+    // material.h:38: metal(a, f) keeps fuzz(f < 1 ? f : 1); dielectrics carry no albedo
+    w.s.push_back({{scene->cx[i], scene->cy[i], scene->cz[i]}, scene->radius[i], (int)k,
+                   k == RT_DIELECTRIC ? d3{1, 1, 1} : alb, k == RT_METAL ? (p < 1 ? p : 1) : p});
+  }
+  return reference_render_world(w, r, {13, 2, 3}, {0, 0, 0}, 0.1, 10.0, width, aspect, spp, max_depth,
+                                rgb_out, segments);
+}
+
+namespace {
+int reference_render_world(dworld &w, rng64 &r, d3 lookfrom, d3 lookat, double aperture, double focus,
+                           int width, double aspect, int spp, int max_depth, uint8_t *rgb_out,
+                           unsigned long long *segments) {
+  const int height = (int)(width / aspect);
   // camera.h:8-26
   const double pi = 3.1415926535897932385;
   double theta = 20.0 * pi / 180.0;
@@ -970,6 +1009,7 @@ int rto_reference_render(int width, double aspect, int spp, int max_depth, int s
   if (segments) *segments = w.calls;
   return 0;
 }
+}  // namespace
 
 int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
                             float *out, double *exact, int no_dither, unsigned long long *segments,

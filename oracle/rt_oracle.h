@@ -14,6 +14,11 @@ extern "C" {
  * rgb_out == NULL: size query (fills *height_out). */
 int rto_reference_render(int width, double aspect, int spp, int max_depth, int scene,
                          uint8_t *rgb_out, int *height_out, unsigned long long *segments);
+/* The same for any scene (the final scene's camera, src/cpu/main.cc:90-97;
+ * no scene draws precede the samples): what the reference harness renders
+ * for a `file:` scene (oracle/ref_harness.cc). */
+int rto_reference_render_view(const rt_scene_view *scene, int width, double aspect, int spp, int max_depth,
+                              uint8_t *rgb_out, int *height_out, unsigned long long *segments);
 /* fp32 restatement of the kernel algorithm; same arguments as rt_render. */
 int rto_kernel_render(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
                       float *out, unsigned long long *segments, int threads);

@@ -458,7 +458,9 @@ void build_accel(const rt_scene_view *s, const accel_options &o, accel_build &a)
     r.ar = glass ? 1.0f : s->albedo_rgb[3 * i + 0];
     r.ag = glass ? 1.0f : s->albedo_rgb[3 * i + 1];
     r.ab = glass ? 1.0f : s->albedo_rgb[3 * i + 2];
-    r.param = s->mat_param[i];
+    // metal fuzz is clamped to 1 as the reference's constructors do
+    // (src/cpu/material.h:38, src/gpu/material.h:45: fuzz(f < 1 ? f : 1))
+    r.param = s->mat_kind[i] == RT_METAL ? std::min(s->mat_param[i], 1.0f) : s->mat_param[i];
     r.kind = s->mat_kind[i];
     r.radius = s->radius[i];
     const double x = s->cx[i], y = s->cy[i], z = s->cz[i], rr = s->radius[i];

@@ -50,6 +50,25 @@ def reference_render(width, aspect, spp, max_depth=50, scene=0):
     return out, seg.value
 
 
+def reference_render_view(scene, width, aspect, spp, max_depth=50):
+    """fp64 restatement of src/cpu on any scene, with the final scene's camera
+    (what oracle/_ref/ref_harness renders for a `file:` scene)
+    -> (uint8 [H, W, 3] top row first, segments)."""
+    L = lib()
+    L.rto_reference_render_view.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                                            ctypes.POINTER(ctypes.c_ulonglong)]
+    v = scene.view()
+    h = ctypes.c_int()
+    assert L.rto_reference_render_view(ctypes.addressof(v), width, aspect, spp, max_depth, None,
+                                       ctypes.byref(h), None) == 0
+    out = np.zeros((h.value, width, 3), np.uint8)
+    seg = ctypes.c_ulonglong()
+    assert L.rto_reference_render_view(ctypes.addressof(v), width, aspect, spp, max_depth, out.ctypes.data,
+                                       ctypes.byref(h), ctypes.byref(seg)) == 0
+    return out, seg.value
+
+
 def kernel_render(scene, cam, params, threads=0):
     """fp32 restatement of the kernel algorithm -> (float32 [rows, W, 3], segments)."""
     import rtow
