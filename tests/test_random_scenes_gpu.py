@@ -1,7 +1,7 @@
 """GPU parity on randomised inputs: the HIP kernel (through the C ABI) against
 the oracle's fp32 kernel-mode restatement, bit for bit, on seeded random
-scenes, cameras, semantics flags, walks, frame sizes, sample counts and
-depths -- the combinations the hand-written cases in test_parity_gpu.py do
+scenes, cameras, semantics flags, walks, frame sizes, sample counts,
+depths and rank shares -- the combinations the hand-written cases in test_parity_gpu.py do
 not enumerate (overlapping and nested spheres, negative-radius glass, metal
 fuzz above 1, index of refraction below 1, lenses, extreme fields of view).
 
@@ -86,8 +86,13 @@ def case(rtow, seed):
     cam = random_camera(rtow, rng, w, h)
     flags = int(rng.choice([0, rtow.RT_FLAG_OPEN_INTERVAL, rtow.RT_FLAG_METAL_UNIT_VECTOR,
                             rtow.RT_FLAG_GPU_SEMANTICS]))
-    p = rtow.make_params(w, h, int(rng.integers(1, 13)), max_depth=int(rng.choice([1, 2, 5, 12, 50])),
-                         seed=int(rng.integers(0, 2 ** 40)), flags=flags, units=int(rng.integers(0, 4)))
+    spp, depth = int(rng.integers(1, 13)), int(rng.choice([1, 2, 5, 12, 50]))
+    seed, units = int(rng.integers(0, 2 ** 40)), int(rng.integers(0, 4))
+    # a rank's share of a multi-GPU frame in a third of the cases
+    world = int(rng.integers(2, 6)) if rng.uniform() < 0.33 else 1
+    rank, row_block = int(rng.integers(0, world)), int(rng.choice([1, 2, 4, 8, 16]))
+    p = rtow.make_params(w, h, spp, max_depth=depth, seed=seed, flags=flags, units=units, rank=rank, world=world,
+                         row_block=row_block)
     return scene, cam, p
 
 
@@ -112,6 +117,7 @@ def test_random_scene_bit_exact_vs_oracle(rtow, gpu_ctx, seed):
             assert n_diff == 0 and st.segments == segs, (
                 f"seed {seed}, walk {name}: {n_diff} floats differ, segments {st.segments} vs {segs}; "
                 f"{scene.n} spheres, {p.width}x{p.height}x{p.spp} depth {p.max_depth} flags {base} "
+                f"band {p.band_offset}/{p.band_stride} x {p.row_block} rows "
                 f"units {p.units} grid {mode} budget {budget} launches {st.launches}")
     finally:
         gpu_ctx.set_option(rtow.RT_OPT_LAUNCH_SAMPLES, 0)
