@@ -49,3 +49,35 @@ def dump_scene_exact(scene, path):
 
 # (width, spp, depth) per case: 16:9 frames, so height = int(width * 9 / 16)
 CASES = [(48 + 8 * (k % 5), 2 + k % 7, (50, 5, 2, 12)[k % 4]) for k in range(24)]
+
+
+def degenerate_scenes(rtow):
+    """Inputs that stress the BVH / layer-grid builder: coincident spheres,
+    spheres on a line, a crowded layer (no grid cell size keeps <= 15 per
+    cell), huge and tiny radii, far-away spheres, and the layer-mode size
+    thresholds.  name -> Scene."""
+    f32 = np.float32
+    rng = np.random.default_rng(99)
+
+    def mk(cx, cy, cz, r, kind=None, param=None):
+        n = len(cx)
+        kind = np.zeros(n, np.uint32) if kind is None else np.asarray(kind, np.uint32)
+        param = np.where(kind == 2, 1.5, 0.3) if param is None else param
+        return rtow.Scene(np.asarray(cx, f32), np.asarray(cy, f32), np.asarray(cz, f32), np.asarray(r, f32),
+                          kind, np.full((n, 3), 0.6, f32), np.asarray(param, f32))
+
+    out = {
+        "coincident_100": mk([0.5] * 100, [0.2] * 100, [0.5] * 100, [0.2] * 100),
+        "line_200": mk(np.linspace(-8, 8, 200), [0.2] * 200, [0.0] * 200, [0.05] * 200),
+        "crowded_layer_300": mk(rng.uniform(-0.5, 0.5, 300), [0.2] * 300, rng.uniform(-0.5, 0.5, 300), [0.2] * 300),
+        "huge_and_tiny": mk([0, 3, -3, 1, 0], [-10000.5, 0.5, 0.5, 0.1, 1], [0, 1, -1, 2, -2],
+                            [10000.0, 1e-3, 2e-3, 0.3, 0.5], kind=[0, 1, 2, 0, 2]),
+        "far_away": mk([1e5, -1e5, 0, 3], [0, 0, 1e5, 0.5], [0, 0, 0, 0], [100, 50, 1e4, 0.5]),
+    }
+    base = rtow.final_scene()
+    for n in (1, 2, 3, 63, 64, 65):
+        idx = np.r_[0, 1 + np.arange(n - 1)] if n > 1 else np.array([0])
+        idx = idx[idx < base.n]
+        out["final_prefix_%d" % n] = rtow.Scene(base.cx[idx], base.cy[idx], base.cz[idx], base.radius[idx],
+                                                base.kind[idx], base.albedo[idx], base.param[idx])
+    return out

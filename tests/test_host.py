@@ -274,6 +274,22 @@ def test_accel_builder_invariants_on_host(rtow):
     assert five["layer_mode"] == 0 and five["grid_items"] == 0
 
 
+def test_accel_builder_on_degenerate_scenes(rtow):
+    """The builder on inputs that stress it (tests/random_scenes.py
+    degenerate_scenes: coincident spheres, a line, a crowded layer, huge and
+    tiny radii, far-away spheres, the layer-mode size thresholds): every grid
+    it builds keeps its invariants, in every placement; the GPU renders of
+    the same scenes are checked against the oracle in test_random_scenes_gpu.py."""
+    import random_scenes
+    for name, scene in random_scenes.degenerate_scenes(rtow).items():
+        for mode in ("auto", "lds", "cells", "global"):
+            info = rtow.accel_info(scene, grid_mode=mode)
+            if info["grid_items"]:
+                assert info["grid_starts_ok"] == 1 and info["grid_ring_empty"] == 1, (name, mode, info)
+                assert 1 <= info["max_items_per_cell"] <= 15, (name, mode, info)
+            assert info["bvh_slots"] >= scene.n, (name, info)
+
+
 @pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="needs hipcc")
 def test_host_code_under_asan_ubsan():
     """tools/host_sanitize.sh: the scene builders, cameras, BVH / grid builder,

@@ -140,3 +140,28 @@ def test_metal_fuzz_above_one_is_clamped_on_the_device(rtow, gpu_ctx):
         gpu_ctx.upload(dataclasses.replace(base, param=param))
         imgs.append(gpu_ctx.render(cam, rtow.make_params(96, 48, 8, seed=3, flags=WALKS["bvh"])))
     assert np.array_equal(imgs[0][0], imgs[1][0]) and imgs[0][1].segments == imgs[1][1].segments
+
+
+DEGENERATE = ["coincident_100", "line_200", "crowded_layer_300", "huge_and_tiny", "far_away", "final_prefix_1",
+              "final_prefix_2", "final_prefix_3", "final_prefix_63", "final_prefix_64", "final_prefix_65"]
+
+
+@pytest.mark.parametrize("name", DEGENERATE)
+def test_degenerate_scene_bit_exact_vs_oracle(rtow, gpu_ctx, name):
+    """The builder's stress inputs (tests/random_scenes.py degenerate_scenes)
+    rendered in all three walks and every grid placement: bit-exact vs the
+    brute-force oracle."""
+    import random_scenes
+    scene = random_scenes.degenerate_scenes(rtow)[name]
+    cam = rtow.camera_cpu(aspect=48 / 27)
+    p = rtow.make_params(48, 27, 6, seed=17)
+    want, segs = kernel_render(scene, cam, p)
+    try:
+        for mode in ("auto", "lds", "cells", "global"):
+            gpu_ctx.upload(scene, grid_mode=mode)
+            for walk in WALKS.values():
+                p.flags = walk
+                got, st = gpu_ctx.render(cam, p)
+                assert np.array_equal(got, want) and st.segments == segs, (name, mode, walk)
+    finally:
+        gpu_ctx.set_option(rtow.RT_OPT_GRID_PLACEMENT, 0)
