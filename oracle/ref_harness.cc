@@ -29,6 +29,8 @@
 //        APERTURE FOCUS_DIST override the camera's lens (depth of field)
 //        PPM (P3) on stdout; on stderr a JSON stats line with samples,
 //        segments (= hittable_list::hit calls), sphere_tests and seconds.
+//   ref_harness hits PATH   -> sphere::hit (t_min 0.001) on the cases in PATH,
+//        one `o[3] d[3] c[3] r` per line, as kat-format JSON lines
 //   ref_harness kat                         -> known-answer vectors (JSON lines)
 // standard headers first so the access override below touches only the
 // reference's own classes
@@ -283,6 +285,34 @@ int cmd_kat() {
   return 0;
 }
 
+// sphere::hit (sphere.h:24-51) on cases read from a file, one per line:
+// o[3] d[3] c[3] r -> one kat-format JSON line each (t_min 0.001, t_max inf)
+int cmd_hits(const char *path) {
+  FILE *f = std::fopen(path, "r");
+  if (!f) return 2;
+  double v[10];
+  while (std::fscanf(f, "%lf %lf %lf %lf %lf %lf %lf %lf %lf %lf", &v[0], &v[1], &v[2], &v[3], &v[4], &v[5],
+                     &v[6], &v[7], &v[8], &v[9]) == 10) {
+    auto mat = make_shared<lambertian>(color(0.5, 0.5, 0.5));
+    sphere s(point3(v[6], v[7], v[8]), v[9], mat);
+    ray r(point3(v[0], v[1], v[2]), vec3(v[3], v[4], v[5]));
+    hit_record rec;
+    const bool h = s.hit(r, 0.001, infinity, rec);
+    std::printf("{\"kind\": \"sphere_hit\", \"o\": [%.17g, %.17g, %.17g], \"d\": [%.17g, %.17g, %.17g], "
+                "\"c\": [%.17g, %.17g, %.17g], \"r\": %.17g, \"hit\": %s",
+                v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], h ? "true" : "false");
+    if (h) {
+      std::printf(", \"t\": %.17g, ", rec.t);
+      pv("p", rec.p); std::printf(", ");
+      pv("normal", rec.normal);
+      std::printf(", \"front_face\": %s", rec.front_face ? "true" : "false");
+    }
+    std::printf("}\n");
+  }
+  std::fclose(f);
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -293,5 +323,6 @@ int main(int argc, char **argv) {
   if (!std::strcmp(argv[1], "scene")) return cmd_scene();
   if (!std::strcmp(argv[1], "render")) return cmd_render(argc, argv);
   if (!std::strcmp(argv[1], "kat")) return cmd_kat();
+  if (!std::strcmp(argv[1], "hits") && argc > 2) return cmd_hits(argv[2]);
   return 2;
 }
