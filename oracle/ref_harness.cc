@@ -31,6 +31,8 @@
 //        segments (= hittable_list::hit calls), sphere_tests and seconds.
 //   ref_harness hits PATH   -> sphere::hit (t_min 0.001) on the cases in PATH,
 //        one `o[3] d[3] c[3] r` per line, as kat-format JSON lines
+//   ref_harness cameras PATH -> the camera basis (camera.h:8-26) for each
+//        `lookfrom[3] lookat[3] vup[3] vfov aspect aperture focus` line of PATH
 //   ref_harness kat                         -> known-answer vectors (JSON lines)
 // standard headers first so the access override below touches only the
 // reference's own classes
@@ -313,6 +315,32 @@ int cmd_hits(const char *path) {
   return 0;
 }
 
+// camera (camera.h:8-26) on parameter sets read from a file, one per line:
+// lookfrom[3] lookat[3] vup[3] vfov aspect aperture focus_dist -> its basis
+int cmd_cameras(const char *path) {
+  FILE *f = std::fopen(path, "r");
+  if (!f) return 2;
+  double v[13];
+  while (std::fscanf(f, "%lf %lf %lf %lf %lf %lf %lf %lf %lf %lf %lf %lf %lf", &v[0], &v[1], &v[2], &v[3], &v[4],
+                     &v[5], &v[6], &v[7], &v[8], &v[9], &v[10], &v[11], &v[12]) == 13) {
+    camera cam(point3(v[0], v[1], v[2]), point3(v[3], v[4], v[5]), vec3(v[6], v[7], v[8]), v[9], v[10], v[11],
+               v[12]);
+    std::printf("{\"kind\": \"camera\", \"args\": [");
+    for (int k = 0; k < 13; ++k) std::printf(k ? ", %.17g" : "%.17g", v[k]);
+    std::printf("], ");
+    pv("origin", cam.origin); std::printf(", ");
+    pv("lower_left_corner", cam.lower_left_corner); std::printf(", ");
+    pv("horizontal", cam.horizontal); std::printf(", ");
+    pv("vertical", cam.vertical); std::printf(", ");
+    pv("u", cam.u); std::printf(", ");
+    pv("v", cam.v); std::printf(", ");
+    pv("w", cam.w);
+    std::printf(", \"lens_radius\": %.17g}\n", cam.lens_radius);
+  }
+  std::fclose(f);
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -324,5 +352,6 @@ int main(int argc, char **argv) {
   if (!std::strcmp(argv[1], "render")) return cmd_render(argc, argv);
   if (!std::strcmp(argv[1], "kat")) return cmd_kat();
   if (!std::strcmp(argv[1], "hits") && argc > 2) return cmd_hits(argv[2]);
+  if (!std::strcmp(argv[1], "cameras") && argc > 2) return cmd_cameras(argv[2]);
   return 2;
 }

@@ -58,6 +58,32 @@ def test_camera_cpu_vs_reference_kat(rtow):
     assert cam.has_lens == 1 and cam.model == 0
 
 
+def test_camera_cpu_vs_reference_random_kat(rtow):
+    """rt_camera_cpu on 200 random parameter sets (eye and target anywhere,
+    tilted vup, vfov 5-150, aspect 0.3-4, aperture 0-2, focus 0.5-50) against
+    the reference's own camera constructor (tests/golden/make_camera_kat.py):
+    every field is the fp32 rounding of the reference's fp64 value."""
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "kat_cameras.jsonl")) as f:
+        kats = [json.loads(line) for line in f]
+    assert len(kats) == 200
+    f32 = lambda v: np.array(v, np.float64).astype(np.float32)
+    for k in kats:
+        a = k["args"]
+        cam = rtow.camera_cpu(lookfrom=a[0:3], lookat=a[3:6], vup=a[6:9], vfov=a[9], aspect=a[10], aperture=a[11],
+                              focus_dist=a[12])
+        assert np.array_equal(np.array(cam.eye[:], np.float32), f32(k["origin"])), k
+        assert np.array_equal(np.array(cam.corner[:], np.float32), f32(k["lower_left_corner"])), k
+        assert np.array_equal(np.array(cam.horiz[:], np.float32), f32(k["horizontal"])), k
+        assert np.array_equal(np.array(cam.vert[:], np.float32), f32(k["vertical"])), k
+        lu = np.array(k["u"]) * k["lens_radius"]
+        lv = np.array(k["v"]) * k["lens_radius"]
+        assert cam.has_lens == (1 if k["lens_radius"] > 0 else 0), k
+        if cam.has_lens:
+            assert np.array_equal(np.array(cam.lens_u[:], np.float32), lu.astype(np.float32)), k
+            assert np.array_equal(np.array(cam.lens_v[:], np.float32), lv.astype(np.float32)), k
+
+
 def test_camera_gpu_model(rtow):
     """new_camera (src/gpu/camera.h:75-109): pixel deltas span the viewport."""
     cam = rtow.camera_gpu(1920, 1080)
