@@ -33,6 +33,7 @@
 //        one `o[3] d[3] c[3] r` per line, as kat-format JSON lines
 //   ref_harness cameras PATH -> the camera basis (camera.h:8-26) for each
 //        `lookfrom[3] lookat[3] vup[3] vfov aspect aperture focus` line of PATH
+//   ref_harness colors PATH  -> write_color's line for each `r g b spp` line
 //   ref_harness kat                         -> known-answer vectors (JSON lines)
 // standard headers first so the access override below touches only the
 // reference's own classes
@@ -341,6 +342,22 @@ int cmd_cameras(const char *path) {
   return 0;
 }
 
+// write_color (color.h:8-23) on sums read from a file, one `r g b spp` per
+// line -> the reference's output line for each
+int cmd_colors(const char *path) {
+  FILE *f = std::fopen(path, "r");
+  if (!f) return 2;
+  double r, g, b;
+  int spp;
+  while (std::fscanf(f, "%lf %lf %lf %d", &r, &g, &b, &spp) == 4) {
+    std::ostringstream os;
+    write_color(os, color(r, g, b), spp);
+    std::fputs(os.str().c_str(), stdout);
+  }
+  std::fclose(f);
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -353,5 +370,6 @@ int main(int argc, char **argv) {
   if (!std::strcmp(argv[1], "kat")) return cmd_kat();
   if (!std::strcmp(argv[1], "hits") && argc > 2) return cmd_hits(argv[2]);
   if (!std::strcmp(argv[1], "cameras") && argc > 2) return cmd_cameras(argv[2]);
+  if (!std::strcmp(argv[1], "colors") && argc > 2) return cmd_colors(argv[2]);
   return 2;
 }

@@ -167,3 +167,17 @@ def ppm_p3_bytes(rgb):
     flat = rgb.reshape(-1, 3)
     body = "".join("%d %d %d\n" % (r, g, b) for r, g, b in flat)
     return ("P3\n%d %d\n255\n" % (w, h) + body).encode()
+
+
+def color_kat():
+    """tests/golden/kat_colors.txt (make_color_kat.py): [(float32 sums[3], spp,
+    reference levels[3])], fp32 sums within a few ulps of write_color's level
+    thresholds."""
+    out = []
+    with open(os.path.join(GOLDEN, "kat_colors.txt")) as f:
+        for line in f:
+            left, right = line.split("|")
+            v = left.split()
+            out.append((np.array([float(x) for x in v[:3]], np.float32), int(v[3]),
+                        [int(x) for x in right.split()]))
+    return out

@@ -84,6 +84,16 @@ def test_camera_cpu_vs_reference_random_kat(rtow):
             assert np.array_equal(np.array(cam.lens_v[:], np.float32), lv.astype(np.float32)), k
 
 
+def test_tonemap_at_level_boundaries_vs_reference_write_color(rtow):
+    """rt_tonemap_u8 (src/cpu mode) on 703 fp32 pixel sums within a few ulps
+    of write_color's level thresholds, spp 1 .. 2^20: the reference's own
+    write_color output (tests/golden/make_color_kat.py) level for level."""
+    from oracle_lib import color_kat
+    for sums, spp, want in color_kat():
+        got = rtow.tonemap(sums.reshape(1, 1, 3), spp)
+        assert [int(x) for x in got.reshape(3)] == want, (sums, spp, want)
+
+
 def test_camera_gpu_model(rtow):
     """new_camera (src/gpu/camera.h:75-109): pixel deltas span the viewport."""
     cam = rtow.camera_gpu(1920, 1080)

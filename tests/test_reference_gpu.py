@@ -208,6 +208,21 @@ def test_device_tonemap_matches_write_color_kat(rtow, gpu_ctx):
         assert " ".join(str(int(v)) for v in got[0]) == k["out"], k
 
 
+def test_device_tonemap_at_level_boundaries(rtow, gpu_ctx):
+    """The device write_color (rt_tonemap_async, src/cpu mode) on 703 fp32
+    sums within a few ulps of the level thresholds: the reference's own
+    write_color levels (tests/golden/make_color_kat.py), all in one launch
+    per spp."""
+    from oracle_lib import color_kat
+    by_spp = {}
+    for sums, spp, want in color_kat():
+        by_spp.setdefault(spp, []).append((sums, want))
+    for spp, rows in by_spp.items():
+        sums = np.stack([r[0] for r in rows]).reshape(-1, 1, 3)
+        got = device_tonemap(rtow, gpu_ctx, sums, spp, 0).reshape(-1, 3)
+        assert np.array_equal(got, np.array([r[1] for r in rows])), spp
+
+
 # ------------------------------------------------------- KAT: device math --
 
 def _kat(kind):
