@@ -924,6 +924,38 @@ int reference_render_world(dworld &w, rng64 &r, d3 lookfrom, d3 lookat, double a
                            unsigned long long *segments);
 }  // namespace
 
+// The kernel's sampling draws on n pcg4d keys (i, 7, 3, seed), for the
+// distribution tests (tests/test_oracle.py): kind 0 a unit vector (lambertian
+// and metal), 1 a point of the unit ball (metal fuzz: ball_radius x unit
+// vector, random_in_unit_sphere's law), 2 a point of the unit disk (the
+// lens, random_in_unit_disk), 3 a lambertian direction about the normal
+// (0, 0, 1), normalised as the kernel does.  3 floats per draw.
+int rto_sample_probe(int kind, uint32_t n, uint32_t seed, float *out) {
+  if (!out || kind < 0 || kind > 3) return -1;
+  for (uint32_t i = 0; i < n; ++i) {
+    const u4 r = pcg4d(i, 7u, 3u, seed);
+    float v[3] = {0, 0, 0};
+    if (kind == 2) {
+      const float rr = sqrt_k(unif(r.z));
+      float s, c;
+      sincos_turn(unif(r.w), s, c);
+      v[0] = rr * c;
+      v[1] = rr * s;
+    } else {
+      unit_vec(unif(r.x), unif(r.y), v[0], v[1], v[2]);
+      if (kind == 1) {
+        const float rho = ball_radius(r);
+        for (float &x : v) x *= rho;
+      } else if (kind == 3) {
+        v[2] += 1.0f;
+        normalize3(v[0], v[1], v[2]);
+      }
+    }
+    for (int a = 0; a < 3; ++a) out[3 * (size_t)i + a] = v[a];
+  }
+  return 0;
+}
+
 int rto_reference_render(int width, double aspect, int spp, int max_depth, int scene,
                          uint8_t *rgb_out, int *height_out, unsigned long long *segments) {
   if (width < 2 || !(aspect > 0) || spp < 1 || max_depth < 0) return -1;

@@ -19,6 +19,9 @@ int rto_reference_render(int width, double aspect, int spp, int max_depth, int s
  * for a `file:` scene (oracle/ref_harness.cc). */
 int rto_reference_render_view(const rt_scene_view *scene, int width, double aspect, int spp, int max_depth,
                               uint8_t *rgb_out, int *height_out, unsigned long long *segments);
+/* The kernel's sampling draws (unit vector, unit-ball point, unit-disk
+ * point, lambertian direction about +z) on n keys: 3 floats each. */
+int rto_sample_probe(int kind, uint32_t n, uint32_t seed, float *out);
 /* fp32 restatement of the kernel algorithm; same arguments as rt_render. */
 int rto_kernel_render(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
                       float *out, unsigned long long *segments, int threads);

@@ -181,3 +181,12 @@ def color_kat():
             out.append((np.array([float(x) for x in v[:3]], np.float32), int(v[3]),
                         [int(x) for x in right.split()]))
     return out
+
+
+def sample_probe(kind, n, seed=1):
+    """The kernel's sampling draws (rto_sample_probe): float32 [n, 3]."""
+    L = lib()
+    L.rto_sample_probe.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+    out = np.zeros((n, 3), np.float32)
+    assert L.rto_sample_probe(kind, n, seed, out.ctypes.data) == 0
+    return out
