@@ -328,6 +328,30 @@ def test_stochastic_rounding_bit_exact_vs_oracle(rtow, gpu_ctx, oracle):
     gpu_ctx.set_option(rtow.RT_OPT_LAUNCH_SAMPLES, 0)
 
 
+def test_strided_ranges_times_sample_ranges_give_the_same_image(rtow, gpu_ctx):
+    """A plan with both splits (rt_api.cpp plan_launches): 256x256 at 1000 spp
+    under a 2^22 budget would leave 62 spp per wave in sample ranges alone,
+    so it runs 4 strided entry ranges x 4 sample ranges of 250 spp; with 3
+    units per tile (about 83 spp per wave in each unit's share) as 16 entry
+    ranges.  Bit-identical to the one-launch render."""
+    gpu_ctx.upload(rtow.final_scene())
+    cam = rtow.camera_cpu(aspect=1.0)
+    p = rtow.make_params(256, 256, 1000, seed=77, flags=GRID, units=1)
+    one, s1 = gpu_ctx.render(cam, p)
+    assert s1.launches == 1
+    try:
+        gpu_ctx.set_option(rtow.RT_OPT_LAUNCH_SAMPLES, 1 << 22)
+        for units in (1, 3):
+            p.units = units
+            plan = rtow.launch_plan(p, 1 << 22)
+            assert (plan["ranges"], plan["chunks"]) == ((4, 4) if units == 1 else (16, 1)), plan
+            img, st = gpu_ctx.render(cam, p)
+            assert st.launches == plan["launches"]
+            assert np.array_equal(img, one) and st.segments == s1.segments, units
+    finally:
+        gpu_ctx.set_option(rtow.RT_OPT_LAUNCH_SAMPLES, 0)
+
+
 def test_bounded_launches_give_the_same_image(rtow, gpu_ctx):
     """a render is split into launches of about
     RT_OPT_LAUNCH_SAMPLES samples at most.  C4's rank-0 share (2048 x 16384
