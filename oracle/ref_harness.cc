@@ -34,6 +34,8 @@
 //   ref_harness cameras PATH -> the camera basis (camera.h:8-26) for each
 //        `lookfrom[3] lookat[3] vup[3] vfov aspect aperture focus` line of PATH
 //   ref_harness colors PATH  -> write_color's line for each `r g b spp` line
+//   ref_harness vectors PATH -> reflect / refract / reflectance for each
+//        `v[3] n[3] eta cosine ref_idx` line
 //   ref_harness kat                         -> known-answer vectors (JSON lines)
 // standard headers first so the access override below touches only the
 // reference's own classes
@@ -358,6 +360,29 @@ int cmd_colors(const char *path) {
   return 0;
 }
 
+// reflect / refract (vec3.h:124-131) and dielectric::reflectance
+// (material.h:82-87) on cases read from a file, one `v[3] n[3] eta cosine
+// ref_idx` per line -> kat-format JSON lines (reflect, refract, reflectance)
+int cmd_vectors(const char *path) {
+  FILE *f = std::fopen(path, "r");
+  if (!f) return 2;
+  double a[9];
+  while (std::fscanf(f, "%lf %lf %lf %lf %lf %lf %lf %lf %lf", &a[0], &a[1], &a[2], &a[3], &a[4], &a[5], &a[6],
+                     &a[7], &a[8]) == 9) {
+    const vec3 v(a[0], a[1], a[2]), n(a[3], a[4], a[5]);
+    std::printf("{\"kind\": \"reflect\", ");
+    pv("v", v); std::printf(", "); pv("n", n); std::printf(", ");
+    pv("out", reflect(v, n)); std::printf("}\n");
+    std::printf("{\"kind\": \"refract\", \"eta\": %.17g, ", a[6]);
+    pv("v", v); std::printf(", "); pv("n", n); std::printf(", ");
+    pv("out", refract(v, n, a[6])); std::printf("}\n");
+    std::printf("{\"kind\": \"reflectance\", \"cosine\": %.17g, \"ref_idx\": %.17g, \"out\": %.17g}\n",
+                a[7], a[8], dielectric::reflectance(a[7], a[8]));
+  }
+  std::fclose(f);
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -371,5 +396,6 @@ int main(int argc, char **argv) {
   if (!std::strcmp(argv[1], "hits") && argc > 2) return cmd_hits(argv[2]);
   if (!std::strcmp(argv[1], "cameras") && argc > 2) return cmd_cameras(argv[2]);
   if (!std::strcmp(argv[1], "colors") && argc > 2) return cmd_colors(argv[2]);
+  if (!std::strcmp(argv[1], "vectors") && argc > 2) return cmd_vectors(argv[2]);
   return 2;
 }
