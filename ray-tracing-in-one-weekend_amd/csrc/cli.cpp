@@ -14,13 +14,16 @@
 //   --width N --height N --spp N --depth N --seed N --spheres K (grid half
 //   extent; 11 = reference, 50 = 10k spheres) --scene final|five
 //   --camera cpu|gpu --semantics cpu|gpu --accel bvh|scan --gpus N --device N
-//   --gather rccl|host --out FILE --p6 --quiet
+//   --devices D0,D1,... --gather rccl|host --out FILE --p6 --quiet
 // With --gpus N > 1 the frame is split into interleaved 8-row bands, one
 // context and stream per device; each device tonemaps its tile to bytes
 // (rt_tonemap_async) and the byte tiles are gathered to device 0 with one
 // RCCL ncclGather over xGMI (single process, ncclCommInitAll); device 0's
 // gathered frame is copied to the host once.  --gather host copies each tile
 // back instead (no RCCL); --gather rccl forces the RCCL path also on 1 GPU.
+// --devices names the device of each band; a device may repeat (bands on one
+// GPU, host gather only: RCCL takes one rank per device), which runs the
+// N-band split, per-band contexts and the assembly on a single-GPU machine.
 #include <fcntl.h>
 #include <unistd.h>
 
@@ -51,6 +54,7 @@ struct options {
   unsigned flags = 0;
   bool bvh = true;  // BVH walk (bit-identical to the scan)
   int gpus = 1, device = 0;
+  std::vector<int> devices;  // --devices: the device of each band (default 0..gpus-1)
   std::string gather = "auto";  // auto: rccl when gpus > 1
   std::string out;
   bool p6 = false, quiet = false;
@@ -70,7 +74,7 @@ void check(int st, const char *what) {
                "usage: %s [--width N] [--height N] [--spp N] [--depth N] [--seed N]\n"
                "          [--spheres HALF_EXTENT] [--scene final|five] [--camera cpu|gpu]\n"
                "          [--semantics cpu|gpu] [--accel bvh|scan] [--gpus N] [--device N]\n"
-               "          [--gather rccl|host] [--out FILE] [--p6] [--quiet]\n",
+               "          [--devices D0,D1,...] [--gather rccl|host] [--out FILE] [--p6] [--quiet]\n",
                argv0);
   std::exit(2);
 }
@@ -113,6 +117,16 @@ int main(int argc, char **argv) {
     else if (a == "--accel") o.bvh = std::string(next()) != "scan";
     else if (a == "--gpus") o.gpus = std::atoi(next());
     else if (a == "--device") o.device = std::atoi(next());
+    else if (a == "--devices") {
+      // one device per band, comma separated; a device may repeat (several
+      // bands rendered by one GPU, each with its own context and stream)
+      o.devices.clear();
+      for (std::string list = next(); !list.empty();) {
+        const size_t c = list.find(',');
+        o.devices.push_back(std::atoi(list.substr(0, c).c_str()));
+        list = c == std::string::npos ? std::string() : list.substr(c + 1);
+      }
+    }
     else if (a == "--gather") o.gather = next();
     else if (a == "--out") o.out = next();
     else if (a == "--p6") o.p6 = true;
@@ -126,6 +140,17 @@ int main(int argc, char **argv) {
   if (gpu_mode && !o.seed_set) o.seed = (unsigned long long)std::time(nullptr);  // main.cu:88
   if (o.width < 2 || o.height < 2 || o.spp < 0 || o.depth < 0 || o.gpus < 1) usage(argv[0]);
   if (o.gather != "auto" && o.gather != "rccl" && o.gather != "host") usage(argv[0]);
+  bool repeated = false;
+  if (!o.devices.empty()) {
+    if ((int)o.devices.size() != o.gpus) usage(argv[0]);
+    for (int g = 0; g < o.gpus; ++g)
+      for (int k = 0; k < g; ++k) repeated |= o.devices[k] == o.devices[g];
+    if (repeated && o.gather == "rccl") {
+      std::fprintf(stderr, "rtow: --gather rccl needs distinct devices\n");
+      std::exit(2);
+    }
+    if (repeated) o.gather = "host";
+  }
 
   // ---- scene (random_scene / new_world) ----
   const uint32_t cap = (uint32_t)(4 * o.half_extent * o.half_extent + 16);
@@ -154,11 +179,16 @@ int main(int argc, char **argv) {
   int ndev = 0;
   check(rt_device_count(&ndev), "rt_device_count");
   if (ndev < 1) die("no HIP device", RT_ERR_NO_DEVICE);
-  if (o.gpus > ndev) {
+  if (o.devices.empty() && o.gpus > ndev) {
     // no silent clamp: a run asked for N GPUs must not report a 1-GPU time as N
     std::fprintf(stderr, "rtow: --gpus %d but only %d HIP device(s) visible\n", o.gpus, ndev);
     std::exit(2);
   }
+  for (int d : o.devices)
+    if (d < 0 || d >= ndev) {
+      std::fprintf(stderr, "rtow: --devices names device %d but only %d HIP device(s) visible\n", d, ndev);
+      std::exit(2);
+    }
 
   // the reference's stderr surface, per personality (src/cpu/main.cc:103-105,
   // src/gpu/main.cu:121-125); our extra lines follow the timing
@@ -200,7 +230,7 @@ int main(int argc, char **argv) {
       p.band_offset = g;
       p.local_rows = (o.height + band_rows - 1) / band_rows * row_block;
     }
-    jobs[g].device = o.gpus == 1 ? o.device : g;
+    jobs[g].device = !o.devices.empty() ? o.devices[g] : o.gpus == 1 ? o.device : g;
     jobs[g].params = p;
   }
   std::vector<rt_context *> ctxs(o.gpus, nullptr);

@@ -71,3 +71,22 @@ def test_cli_depth_and_spp_flags_reach_the_render(rtow):
     r = subprocess.run(args, capture_output=True, timeout=120, check=True)
     got = read_ppm_bytes(r.stdout)
     assert np.array_equal(got, expected(rtow, "cpu_ray_tracer", [], w, h, 1, 1, 2))
+
+
+@pytest.mark.parametrize("devices", ["0,0", "0,0,0", "0,0,0,0,0"])
+def test_cli_multi_band_assembly_on_one_device(rtow, devices):
+    """The --gpus N frame split (interleaved 8-row bands, one context and
+    stream per band, per-band write_color, host gather, row assembly) with
+    every band on device 0: the assembled PPM equals the oracle's whole frame
+    byte for byte.  Heights that are not a multiple of 8 x N leave the last
+    band short and some bands empty."""
+    n = devices.count(",") + 1
+    w, h, spp, seed = 48, 37, 4, 5
+    args = [os.path.join(BIN, "cpu_ray_tracer"), "--width", str(w), "--height", str(h), "--spp", str(spp),
+            "--seed", str(seed), "--gpus", str(n), "--devices", devices]
+    r = subprocess.run(args, capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    err = r.stderr.decode()
+    assert f"Number of GPUs = {n}" in err and "gather (none)" in err
+    assert np.array_equal(read_ppm_bytes(r.stdout), expected(rtow, "cpu_ray_tracer", [], w, h, spp, 50, seed))
+

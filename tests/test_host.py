@@ -291,6 +291,18 @@ def test_cli_no_device_exit_99():
     assert r.returncode == 99  # src/gpu/cuda_utility.h:16
 
 
+@pytest.mark.parametrize("extra,msg", [
+    (["--gpus", "2", "--devices", "0,0", "--gather", "rccl"], b"distinct devices"),
+    (["--gpus", "3", "--devices", "0,0"], b"usage:"),
+])
+def test_cli_devices_argument_checks(extra, msg):
+    """--devices is checked before any device is touched: one entry per band,
+    and no RCCL gather over a repeated device (one rank per device)."""
+    exe = os.path.join(ROOT, "ray-tracing-in-one-weekend_amd", "bin", "cpu_ray_tracer")
+    r = subprocess.run([exe, "--width", "16", "--quiet"] + extra, capture_output=True, timeout=60)
+    assert r.returncode == 2 and msg in r.stderr
+
+
 def test_accel_builder_invariants_on_host(rtow):
     """rt_internal_accel_info runs rt_scene_upload's BVH / layer-grid builder on
     the host: the final scene is a layer scene whose grid fits the LDS budget of
