@@ -164,8 +164,15 @@ def roofline(work, k_avg_s, accel, pmc, pmc_reason, device_sha):
     flops = work["sphere_tests"] * FLOPS_PER_TEST + work["box_tests"] * (
         FLOPS_PER_CELL if accel == "bvh" else FLOPS_PER_BOX)
     achieved = flops / k_avg_s / 1e12
-    # the counters are only valid for the device code they were collected on
+    # the counters are only valid for the device code they were collected on:
+    # a summary of other kernel code keeps its name and hash in the line, but
+    # every field derived from it is null (Weak 4)
     pmc_fresh = bool(pmc) and pmc.get("device_code_sha16") == device_sha
+    pmc_src = os.path.relpath(pmc["path"], ROOT) if pmc.get("path") else None
+    if pmc and not pmc_fresh:
+        pmc_reason = (f"{pmc_src or 'the PMC summary'} was collected on device code "
+                      f"{pmc.get('device_code_sha16')}, this build is {device_sha}: its counters are not used")
+        pmc = {}
     valu_insts = pmc.get("valu_insts_per_launch")
     cnt = pmc.get("counters_avg_per_dispatch", {})
     traffic = pmc.get("hbm_bytes_per_launch")
@@ -204,7 +211,7 @@ def roofline(work, k_avg_s, accel, pmc, pmc_reason, device_sha):
                      "peak_GBps": PEAK_HBM_GBPS,
                      "frac": round(traffic / k_avg_s / 1e9 / PEAK_HBM_GBPS, 5)}
                     if traffic else None),
-            "pmc_source": os.path.relpath(pmc["path"], ROOT) if pmc.get("path") else None,
+            "pmc_source": pmc_src,
             "pmc_matches_device_code": pmc_fresh,
             "pmc_null_reason": pmc_reason,
             "culling_speedup": round(work["bf_tests"] / max(1, work["sphere_tests"]), 1),

@@ -142,8 +142,13 @@ typedef struct {
 } rt_params;
 
 /* Pixel sums (part of the result, like the RNG): a sample's radiance v (at
- * most 1: albedos must lie in [0, 1]) adds q(v * 2^F) to its pixel's uint32
- * sum, F = 31 - floor(log2(spp)); the frame holds sum * 2^-F.  q truncates
+ * most 1 when every albedo lies in [0, 1]) adds q(v * 2^F) to its pixel's
+ * uint32 sum, F = 31 - floor(log2(spp)); the frame holds sum * 2^-F.  A scene
+ * with an albedo A > 1 (energy-creating, as the reference allows) uses 64-bit
+ * sums: v is clamped at vcap = min(A^(max_depth-1), 2^24) and F = 62 -
+ * floor(log2(spp)) - ceil(log2(vcap)); since vcap >= 2^24 > spp whenever the
+ * clamp acts, a clamped sample alone makes its pixel white in write_color, so
+ * only the fp32 sums of such saturated pixels differ from an unclamped sum.  q truncates
  * for spp < 4096 (F >= 20: a bias below 2^-20 per sample, under 0.03 of a
  * tonemap level on the darkest visible pixel) and rounds stochastically for
  * 4096 <= spp < 2^24, trunc(x) + (frac(x) > u) with u a uniform draw keyed by
@@ -151,8 +156,7 @@ typedef struct {
  * not depend on the order, so samples can be traced by any lanes, waves
  * (rt_params.units), launches or GPUs without changing a single bit of the
  * image.  The reference sums in fp64 (src/cpu/main.cc:114-119) or fp32
- * (src/gpu/camera.h:189-194) with no such format and accepts any albedo;
- * rt_scene_upload's [0, 1] albedo range is the one deliberate narrowing.
+ * (src/gpu/camera.h:189-194) with no such format.
  * RT_CHUNK_SPP is kept for source compatibility (ABI 1 summed fp32 in chunks
  * of 64 samples; ABI 2 was never released); nothing depends on it any more. */
 #define RT_CHUNK_SPP 64
@@ -229,12 +233,16 @@ typedef enum {
   RT_OPT_BVH_SIDE = 5,        /* SAH weight of the x- and z-facing sides (default 1) */
   /* about this many samples (pixels x samples per pixel) per render kernel
    * launch at most (default 2^32): a render is split into launches that each
-   * stay well under a second (no monolithic launch).  A launch
-   * runs a range of whole 4-tile blocks (at least 8192 of them, or the whole
-   * frame) with all of their samples; only when such a range is still over
-   * the budget are its samples split into sample ranges as well (a launch
-   * then holds at least one sample per pixel).  At most 65536 launches per
-   * render: a smaller budget is raised to total samples / 65536. */
+   * stay well under a second (no monolithic launch).  The render's
+   * work entries (4-tile blocks x units) are first split by samples: `chunks`
+   * launches over every entry, each tracing spp / chunks samples per pixel.
+   * When that would leave a wave fewer than 100 samples per pixel, the
+   * entries are split as well, into `ranges` strided subsets (range r runs
+   * entries r, r + ranges, r + 2 ranges, ... of the block order, however few
+   * that is), and the samples into chunks of about 250 per wave; a launch
+   * holds at least one sample per pixel.  At most 65536 launches per render:
+   * a smaller budget is raised to total samples / 65536.
+   * rt_internal_launch_plan shows the plan. */
   RT_OPT_LAUNCH_SAMPLES = 6
 } rt_option;
 enum { RT_GRID_AUTO = 0, RT_GRID_LDS = 1, RT_GRID_CELLS_LDS = 2, RT_GRID_GLOBAL = 3 };
@@ -244,11 +252,12 @@ int rt_context_set_option(rt_context *ctx, int option, double value);
  * builds the BVH.  Replaces new_world<<<1,1>>> (src/gpu/main.cu:18-75).
  * Synchronises the device first: renders still running on any stream keep
  * the previous scene.  Centres must be finite, radii finite and non-zero,
- * and the albedos of lambertian and metal spheres in [0, 1] (RT_ERR_INVALID
- * otherwise: the fixed-point pixel sums need a sample's radiance <= 1 -- a
- * deliberate narrowing of the reference, which renders energy-creating
- * albedos too; every scene of the reference is inside it).  Metal fuzz above
- * 1 is clamped to 1, as the reference's metal constructors do
+ * and the albedos of lambertian and metal spheres finite and >= 0
+ * (RT_ERR_INVALID otherwise: a negative albedo gives the reference's
+ * write_color a NaN).  Albedos above 1 are accepted, as the reference's
+ * constructors accept them (src/cpu/material.h:17,38): renders of such a
+ * scene use 64-bit pixel sums (see rt_params).  Metal fuzz above 1 is
+ * clamped to 1, as the reference's metal constructors do
  * (src/cpu/material.h:38, src/gpu/material.h:45). */
 int rt_scene_upload(rt_context *ctx, const rt_scene_view *scene);
 
@@ -357,6 +366,12 @@ int rt_internal_accel_info(const rt_scene_view *scene, int grid_placement, doubl
  * For tests. */
 #define RT_LAUNCH_PLAN_N 5
 int rt_internal_launch_plan(const rt_params *params, double launch_samples, uint64_t *out, size_t n_out);
+
+/* Host only (no device): for each sphere of `scene`, 1 if the kernel's
+ * opaque-inside rule applies to it (a sealed lambertian sphere: no other
+ * ball overlaps its ball), else 0.  Writes
+ * min(n_out, scene->n) bytes.  For tests. */
+int rt_internal_sealed(const rt_scene_view *scene, uint8_t *out, size_t n_out);
 
 #ifdef __cplusplus
 }

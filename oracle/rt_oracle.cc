@@ -356,6 +356,8 @@ void normalize3(float &x, float &y, float &z) {
 struct kscene {
   std::vector<float> cx, cy, cz, ks, inv_r, radius, ar, ag, ab, param, inv_param, r0;
   std::vector<uint32_t> kind;
+  std::vector<uint8_t> sealed;  // the opaque-inside rule applies (sealed_of)
+  double max_albedo = 0.0;      // largest lambertian / metal albedo channel
 };
 
 struct kctx {
@@ -419,11 +421,25 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
   acc[0] = acc[1] = acc[2] = 0.0f;
   double ex[3] = {0.0, 0.0, 0.0};
   if (k.p->max_depth <= 0 || k.p->spp <= 0) return 0;  // ray_color(.., 0) is black, no hit test
+  // the sum format (rt_api.cpp sum_format): albedos above 1 make 64-bit sums
+  // with a radiance clamp vcap = min(A^(max_depth - 1), 2^24) rounded down to
+  // fp32, F = 62 - floor(log2 spp) - ceil(log2 vcap)
   int f = 31;
   for (int s = k.p->spp; s > 1; s >>= 1) --f;
+  const bool wide = sc.max_albedo > 1.0;
+  float vcap = 1.0f;
+  if (wide) {
+    double v = k.p->max_depth > 1 ? std::pow(sc.max_albedo, (double)(k.p->max_depth - 1)) : 1.0;
+    v = std::min(std::max(v, 1.0), 16777216.0);
+    vcap = (float)v;
+    if ((double)vcap > v) vcap = std::nextafter(vcap, 0.0f);
+    int e = 0;
+    const double m = std::frexp((double)vcap, &e);
+    f += 31 - (m == 0.5 ? e - 1 : e);
+  }
   const float qscale = std::ldexp(1.0f, f), qinv = std::ldexp(1.0f, -f);
   const bool dither = f < 20 && !k.no_dither;
-  uint32_t q[3] = {0u, 0u, 0u};
+  uint64_t q[3] = {0u, 0u, 0u};
   for (uint32_t sample = 0; sample < (uint32_t)k.p->spp; ++sample) {
     float o[3], d[3];
     camera_ray(k, pix, col, grow, sample, o, d);
@@ -544,8 +560,9 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
         const float v[3] = {th[0] * fmaf_(a, 0.5f, s0), th[1] * fmaf_(a, 0.7f, s0), th[2] * (s0 + a)};
         const float u = dither ? dither_u(pix, sample, k.seed32) : 0.0f;
         for (int j = 0; j < 3; ++j) {
-          const float x = v[j] * qscale;
-          q[j] += (uint32_t)x + (dither && x - std::floor(x) > u ? 1u : 0u);
+          const float x = (wide ? std::fmin(v[j], vcap) : v[j]) * qscale;
+          const uint64_t qx = wide ? (uint64_t)x : (uint64_t)(uint32_t)x;
+          q[j] += qx + (dither && x - std::floor(x) > u ? 1u : 0u);
           ex[j] += (double)v[j];
         }
         break;
@@ -605,10 +622,12 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
           for (int a = 0; a < 3; ++a) sd[a] = fmaf_(m, nn[a], q[a]);
         }
       }
-      // an opaque sphere hit from inside ends the path:
-      // inside a lambertian or metal sphere every scatter points inward, so
-      // the reference's path would stay inside to the depth cap (black)
-      scattered = scattered && (front || sc.kind[b] == RT_DIELECTRIC);
+      // the opaque-inside rule: a sealed lambertian
+      // sphere hit at its exiting root ends the path (in the reference's
+      // arithmetic every later chord inside it is t = |r|, to the depth cap)
+      if (sc.kind[b] == RT_LAMBERTIAN && sc.sealed[b] && !near) scattered = false;
+      if (wide)  // albedos above 1: the throughput stays finite (the kernel's clamp)
+        for (int a = 0; a < 3; ++a) th[a] = std::fmin(th[a], 0x1p100f);
       ++depth;
       if (!scattered || depth >= k.p->max_depth) break;
       for (int a = 0; a < 3; ++a) {
@@ -618,7 +637,7 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
       normalize3(d[0], d[1], d[2]);
     }
   }
-  for (int a = 0; a < 3; ++a) acc[a] = (float)q[a] * qinv;
+  for (int a = 0; a < 3; ++a) acc[a] = (wide ? (float)q[a] : (float)(uint32_t)q[a]) * qinv;
   if (k.exact) {
     double *e = k.exact + 3 * ((size_t)(&acc[0] - k.out0) / 3);
     for (int a = 0; a < 3; ++a) e[a] = ex[a];
@@ -743,6 +762,7 @@ unsigned long long gpuref_pixel(const kctx &k, int col, int grow, float acc[3], 
       float tbest = INFINITY;
       gvec p{}, nrm{};
       bool front = true;
+      bool inside = false;  // the winner was taken at its exiting root (specification only)
       if (naive) {
         // hittable_list::hit (hittable_list.h:49-65) over sphere::hit (sphere.h:15-44)
         const float a = gdot(d, d);
@@ -822,6 +842,7 @@ unsigned long long gpuref_pixel(const kctx &k, int col, int grow, float acc[3], 
           p = gfma(t, d, o);
           nrm = gvec{(p.x - sc.cx[b]) * sc.inv_r[b], (p.y - sc.cy[b]) * sc.inv_r[b], (p.z - sc.cz[b]) * sc.inv_r[b]};
           front = near != (sc.inv_r[b] < 0.0f);
+          inside = !near;
           if (!front) nrm = gvec{-nrm.x, -nrm.y, -nrm.z};
         }
       }
@@ -846,14 +867,14 @@ unsigned long long gpuref_pixel(const kctx &k, int col, int grow, float acc[3], 
         sd = gadd(nrm, unit_vector());
         const float e = 1e-8f;
         if (std::fabs(sd.x) < e && std::fabs(sd.y) < e && std::fabs(sd.z) < e) sd = nrm;
-        if (!naive && !front) scattered = false;  // the specification's opaque-inside rule
+        if (!naive && inside && sc.sealed[b]) scattered = false;  // the specification's opaque-inside rule
       } else if (sc.kind[b] == RT_METAL) {  // material.h:42-64
         const gvec ud = unnorm ? gunit(d) : d;
         const float kk = -2.0f * gdot(ud, nrm);
         const gvec refl = gfma(kk, nrm, ud);
         const gvec u = unit_vector();
         sd = gfma(sc.param[b], u, refl);
-        scattered = gdot(sd, nrm) > 0.0f && (naive || front);
+        scattered = gdot(sd, nrm) > 0.0f;
       } else {  // material.h:66-104
         const float ratio = front ? sc.inv_param[b] : sc.param[b];
         const gvec ud = unnorm ? gunit(d) : d;
@@ -888,8 +909,31 @@ unsigned long long gpuref_pixel(const kctx &k, int col, int grow, float acc[3], 
   return segs;
 }
 
+// The opaque-inside rule's sealed spheres (restates rt_accel.cpp
+// sealed_spheres): lambertian, |r| > 2 t_min, and no
+// other sphere's ball overlaps its ball (fp64; touching at one point allowed).
+// Brute force over all pairs, independent of the product's sweep.
+std::vector<uint8_t> sealed_of(const rt_scene_view &v) {
+  std::vector<uint8_t> over(v.n, 0), out(v.n, 0);
+  for (uint32_t i = 0; i < v.n; ++i)
+    for (uint32_t j = i + 1; j < v.n; ++j) {
+      const double dx = (double)v.cx[i] - v.cx[j];
+      const double rs = std::fabs((double)v.radius[i]) + std::fabs((double)v.radius[j]);
+      if (std::fabs(dx) >= rs) continue;
+      const double dy = (double)v.cy[i] - v.cy[j], dz = (double)v.cz[i] - v.cz[j];
+      if (dx * dx + dy * dy + dz * dz < rs * rs) over[i] = over[j] = 1;
+    }
+  for (uint32_t i = 0; i < v.n; ++i)
+    out[i] = v.mat_kind[i] == RT_LAMBERTIAN && !over[i] && std::fabs((double)v.radius[i]) > 0.002;
+  return out;
+}
+
 kscene make_kscene(const rt_scene_view &v) {
   kscene s;
+  s.sealed = sealed_of(v);
+  for (uint32_t i = 0; i < v.n; ++i)
+    for (int a = 0; a < 3 && v.mat_kind[i] != RT_DIELECTRIC; ++a)
+      s.max_albedo = std::max(s.max_albedo, (double)v.albedo_rgb[3 * i + a]);
   for (uint32_t i = 0; i < v.n; ++i) {
     const double x = v.cx[i], y = v.cy[i], z = v.cz[i], r = v.radius[i];
     s.cx.push_back(v.cx[i]);
@@ -923,6 +967,13 @@ int reference_render_world(dworld &w, rng64 &r, d3 lookfrom, d3 lookat, double a
                            int width, double aspect, int spp, int max_depth, uint8_t *rgb_out,
                            unsigned long long *segments);
 }  // namespace
+
+int rto_sealed(const rt_scene_view *scene, uint8_t *out) {
+  if (!scene || !out) return -1;
+  const std::vector<uint8_t> v = sealed_of(*scene);
+  std::copy(v.begin(), v.end(), out);
+  return 0;
+}
 
 // The kernel's sampling draws on n pcg4d keys (i, 7, 3, seed), for the
 // distribution tests (tests/test_oracle.py): kind 0 a unit vector (lambertian

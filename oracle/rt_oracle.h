@@ -44,6 +44,8 @@ int rto_trace(const rt_scene_view *scene, const rt_camera *cam, const rt_params 
               int grow, long sample);
 int rto_reference_scene(int half_extent, double *rows, size_t capacity, size_t *n_out,
                         double *rng_next);
+/* the kernel specification's sealed spheres (opaque-inside rule), one byte each */
+int rto_sealed(const rt_scene_view *scene, uint8_t *out);
 #ifdef __cplusplus
 }
 #endif

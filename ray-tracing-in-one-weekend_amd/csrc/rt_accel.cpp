@@ -419,11 +419,49 @@ void fill_slot(pair_geom &g, int l, const rt_scene_view *s, int i) {
 
 }  // namespace
 
+// Sealed spheres (the opaque-inside rule).  A lambertian
+// sphere of radius |r| > 2 t_min whose ball no other sphere's ball overlaps
+// (touching at one point is allowed: the final scene's glass sphere rests on
+// the ground, |C_a - C_b| = r_a + r_b exactly).  In the reference's arithmetic a path inside such
+// a sphere never leaves: its lambertian scatter off the inner wall is n + u
+// (|u| = 1, src/cpu/material.h:19-30, src/gpu/material.h:20-40), so |d| = 2
+// cos(angle to n) and the chord to the far wall is 2 |r| cos / |d| = |r| in
+// the ray's own units -- always past t_min -- and no other surface lies
+// inside the ball.  The path then hits the same sphere again and again until
+// the depth cap and returns black; the kernel ends it black at its first
+// inner hit.  Metal is not sealed (a reflection keeps the entering chord,
+// which may be shorter than t_min), and a ball that another ball overlaps has
+// exits through that sphere (a glass sphere half-embedded in it refracts the
+// path out).  fp64 on the fp32 scene; sweep over x-intervals, O(n log n + overlapping x-pairs).
+void sealed_spheres(const rt_scene_view *s, std::vector<uint8_t> &out) {
+  const uint32_t n = s->n;
+  out.assign(n, 0);
+  std::vector<uint8_t> overlapped(n, 0);
+  std::vector<uint32_t> ord(n);
+  for (uint32_t i = 0; i < n; ++i) ord[i] = i;
+  auto lo = [&](uint32_t i) { return (double)s->cx[i] - std::fabs((double)s->radius[i]); };
+  std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return lo(a) < lo(b) || (lo(a) == lo(b) && a < b); });
+  for (uint32_t k = 0; k < n; ++k) {
+    const uint32_t i = ord[k];
+    const double ri = std::fabs((double)s->radius[i]), hi = (double)s->cx[i] + ri;
+    for (uint32_t m = k + 1; m < n && lo(ord[m]) < hi; ++m) {
+      const uint32_t j = ord[m];
+      const double dx = (double)s->cx[i] - s->cx[j], dy = (double)s->cy[i] - s->cy[j],
+                   dz = (double)s->cz[i] - s->cz[j];
+      const double rs = ri + std::fabs((double)s->radius[j]);
+      if (dx * dx + dy * dy + dz * dz < rs * rs) overlapped[i] = overlapped[j] = 1;
+    }
+  }
+  for (uint32_t i = 0; i < n; ++i)
+    out[i] = s->mat_kind[i] == RT_LAMBERTIAN && !overlapped[i] && std::fabs((double)s->radius[i]) > 0.002 ? 1 : 0;
+}
+
 // What rt_scene_upload (and rt_internal_accel_info) accept: arrays present,
-// known materials, finite centres and radii, non-zero radii, and albedos in
-// [0, 1] (energy-conserving materials: a sample's radiance is then at most 1,
-// which the fixed-point pixel sums rely on; dielectrics
-// ignore theirs).  The builder's sorts need finite keys.
+// known materials, finite centres and radii, non-zero radii, and finite
+// albedos >= 0 (dielectrics ignore theirs).  Albedos above 1 (energy-creating,
+// as the reference's constructors allow, src/cpu/material.h:17,38) switch the
+// render to 64-bit pixel sums; negative ones give the
+// reference's write_color a NaN.  The builder's sorts need finite keys.
 bool scene_ok(const rt_scene_view *s) {
   if (!s || (s->n && (!s->cx || !s->cy || !s->cz || !s->radius || !s->mat_kind || !s->mat_param ||
                       !s->albedo_rgb)))
@@ -433,9 +471,16 @@ bool scene_ok(const rt_scene_view *s) {
         !std::isfinite(s->cx[i]) || !std::isfinite(s->cy[i]) || !std::isfinite(s->cz[i]))
       return false;
     for (int k = 0; k < 3 && s->mat_kind[i] != RT_DIELECTRIC; ++k)
-      if (!(s->albedo_rgb[3 * i + k] >= 0.0f && s->albedo_rgb[3 * i + k] <= 1.0f)) return false;
+      if (!(s->albedo_rgb[3 * i + k] >= 0.0f && std::isfinite(s->albedo_rgb[3 * i + k]))) return false;
   }
   return true;
+}
+
+double max_albedo(const rt_scene_view *s) {
+  double a = 0.0;
+  for (uint32_t i = 0; i < s->n; ++i)
+    for (int k = 0; k < 3 && s->mat_kind[i] != RT_DIELECTRIC; ++k) a = std::max(a, (double)s->albedo_rgb[3 * i + k]);
+  return a;
 }
 
 
@@ -447,6 +492,8 @@ void build_accel(const rt_scene_view *s, const accel_options &o, accel_build &a)
   a.scan_geom.assign(a.n_pad / 2, pair_geom{});
   for (uint32_t i = 0; i < a.n_pad; ++i) fill_slot(a.scan_geom[i / 2], i & 1, s, i < n ? (int)i : -1);
   a.shade.assign(n, shade_rec{});
+  std::vector<uint8_t> sealed;
+  sealed_spheres(s, sealed);
   for (uint32_t i = 0; i < n; ++i) {
     shade_rec &r = a.shade[i];
     std::memset(&r, 0, sizeof r);
@@ -469,6 +516,7 @@ void build_accel(const rt_scene_view *s, const accel_options &o, accel_build &a)
     r.inv_param = (float)(1.0 / ior);
     const double r0 = (1.0 - ior) / (1.0 + ior);
     r.r0 = (float)(r0 * r0);
+    r.sealed = sealed[i];
   }
   bvh_builder bb;
   bb.max_leaf = std::max(1, std::min(bvh_builder::kLeaf, o.bvh_leaf));
@@ -482,21 +530,22 @@ void build_accel(const rt_scene_view *s, const accel_options &o, accel_build &a)
   // until they fit (at most 1.6x the requested side), item indices < 2^16;
   // else global memory.
   int place = kGridGlobal;
+  const size_t lds_max = o.wide ? kGridLdsMaxWide : kGridLdsMax;
   const auto n_items = [&] { return (long long)(bb.grid_items.size() / 4); };
   const auto n_cells = [&] { return (long long)bb.grid_cells.size(); };
   if (!bb.grid_cells.empty()) {
-    const bool lds_fits = n_items() < 4096 && grid_lds_bytes(kGridLds, n_items(), n_cells()) <= kGridLdsMax;
+    const bool lds_fits = n_items() < 4096 && grid_lds_bytes(kGridLds, n_items(), n_cells()) <= lds_max;
     if ((o.grid_placement < 0 || o.grid_placement == kGridLds) && lds_fits) {
       place = kGridLds;
     } else if (o.grid_placement < 0 || o.grid_placement == kGridCells) {
       const double scale0 = bb.grid_scale;
       for (int k = 0; k < 8 && !bb.grid_cells.empty(); ++k) {
         const size_t need = grid_lds_bytes(kGridCells, n_items(), n_cells());
-        if (need <= kGridLdsMax && n_items() < 65536) {
+        if (need <= lds_max && n_items() < 65536) {
           place = kGridCells;
           break;
         }
-        const double grow = std::max(1.02, 1.01 * std::sqrt((double)need / (double)kGridLdsMax));
+        const double grow = std::max(1.02, 1.01 * std::sqrt((double)need / (double)lds_max));
         if (bb.grid_scale * grow > 1.6 * scale0) break;
         bb.grid_scale *= grow;
         bb.build_grid(s, bb.n_layer);

@@ -20,6 +20,7 @@ struct accel_options {
   double side = 1.0;         // RT_OPT_BVH_SIDE
   double grid_scale = 1.0;   // RT_OPT_GRID_SCALE
   int grid_placement = -1;   // RT_OPT_GRID_PLACEMENT: -1 auto, else kGridGlobal / kGridLds / kGridCells
+  bool wide = false;         // 64-bit pixel sums (an albedo above 1): less LDS for the grid
 };
 
 // everything rt_scene_upload copies to the device, plus the builder's facts
@@ -45,8 +46,13 @@ struct accel_build {
 };
 
 // arrays present, known materials, finite centres and radii, non-zero radii,
-// albedos in [0, 1] (rt_scene_upload's contract, include/rt.h)
+// finite albedos >= 0 (rt_scene_upload's contract, include/rt.h)
 bool scene_ok(const rt_scene_view *s);
+// the largest lambertian / metal albedo channel (0 if none): above 1 the
+// render needs 64-bit pixel sums (rt_api.cpp sum_format)
+double max_albedo(const rt_scene_view *s);
+// per sphere: 1 if the opaque-inside rule applies to it (sealed lambertian ball)
+void sealed_spheres(const rt_scene_view *s, std::vector<uint8_t> &out);
 void build_accel(const rt_scene_view *s, const accel_options &o, accel_build &out);
 
 }  // namespace rtk

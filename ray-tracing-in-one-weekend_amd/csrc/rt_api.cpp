@@ -72,6 +72,11 @@ struct rt_context {
   float tonemap_thr32[257];
   double *d_thr64 = nullptr;
   float *d_thr32 = nullptr;
+  // the scene's largest lambertian / metal albedo: above 1, 64-bit pixel sums
+  // (sum_format), with a 64-bit scratch frame for atomic renders
+  double max_albedo = 0.0;
+  uint64_t *d_wide = nullptr;
+  size_t wide_n = 0;
   // rt_context_set_option
   rtk::accel_options opt;
   double launch_samples = rtk::kLaunchSamples;
@@ -139,6 +144,7 @@ void free_scene(rt_context *c) {
   c->layer_mode = false;
   c->extra_pair0 = c->n_extra_pairs = 0;
   c->order_key.clear();  // the pilot's tile costs belong to the old scene
+  c->max_albedo = 0.0;
 }
 
 template <class T>
@@ -154,6 +160,33 @@ int sum_bits(int spp) {
   int f = 31;
   for (int s = spp; s > 1; s >>= 1) --f;
   return f;
+}
+
+// The pixel sums' format (the oracle restates it).
+// Albedos in [0, 1]: a sample's radiance is at most 1; uint32 sums, F = 31 -
+// floor(log2 spp).  An albedo A above 1 (the reference accepts any,
+// src/cpu/material.h:17,38): radiance up to A^(max_depth - 1), so 64-bit sums
+// with vcap = min(A^(max_depth - 1), 2^24) (rounded down to fp32), a sample's
+// radiance clamped at vcap, and F = 62 - floor(log2 spp) - ceil(log2 vcap)
+// (spp samples of at most vcap 2^F, +1 each for the dither, fit 64 bits; F >=
+// 14).  vcap >= 2^24 > spp whenever the clamp can act: a clamped sample alone
+// makes its pixel's mean >= 1, white in either write_color, so the image is
+// the reference's; only the fp32 sums of such pixels saturate.
+struct sum_fmt {
+  bool wide;
+  int f;
+  float vcap;
+};
+sum_fmt sum_format(int spp, int max_depth, double max_albedo) {
+  if (!(max_albedo > 1.0)) return {false, sum_bits(spp), 1.0f};
+  double v = max_depth > 1 ? std::pow(max_albedo, (double)(max_depth - 1)) : 1.0;
+  v = std::min(std::max(v, 1.0), 16777216.0);
+  float vc = (float)v;
+  if ((double)vc > v) vc = std::nextafter(vc, 0.0f);
+  int e = 0;
+  const double m = std::frexp((double)vc, &e);  // vc = m 2^e, m in [0.5, 1)
+  const int ceil_log2 = m == 0.5 ? e - 1 : e;
+  return {true, sum_bits(spp) + 31 - ceil_log2, vc};
 }
 
 }  // namespace
@@ -217,6 +250,7 @@ void rt_context_destroy(rt_context *c) {
   (void)hipFree(c->d_counters);
   (void)hipFree(c->d_frame);
   (void)hipFree(c->d_order);
+  (void)hipFree(c->d_wide);
   (void)hipFree(c->d_thr64);
   (void)hipFree(c->d_thr32);
   for (hipEvent_t ev : c->ev_launch) (void)hipEventDestroy(ev);
@@ -265,7 +299,9 @@ int rt_context_set_option(rt_context *c, int option, double v) {
 int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
   if (!c || !rtk::scene_ok(s)) return RT_ERR_INVALID;
   rtk::accel_build a;
-  rtk::build_accel(s, c->opt, a);
+  rtk::accel_options o = c->opt;
+  o.wide = rtk::max_albedo(s) > 1.0;
+  rtk::build_accel(s, o, a);
 
   RT_HIP(hipSetDevice(c->device));
   // renders enqueued on caller streams may still read the old scene
@@ -288,6 +324,7 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
     return hip_fail(e);
   }
   c->n_spheres = a.n;
+  c->max_albedo = rtk::max_albedo(s);
   c->n_pad = a.n_pad;
   c->n_nodes = (uint32_t)a.per_order;  // nodes holds 8 orders of this many
   c->n_bvh_slots = (uint32_t)a.slots.size();
@@ -479,7 +516,8 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
   const unsigned blocks = (unsigned)((tiles + rtk::kWavesPerBlock - 1) / rtk::kWavesPerBlock);
   const bool grid = c->d_grid_cells && !(prm->flags & RT_FLAG_LAYER_BVH);
   const int place = grid ? c->grid_placement : rtk::kGridGlobal;
-  const int v = ((prm->flags & RT_FLAG_OPEN_INTERVAL) ? rtk::kVarOpen : 0) |
+  const sum_fmt fmt = sum_format(prm->spp, prm->max_depth, c->max_albedo);
+  const int v = (fmt.wide ? rtk::kVarWide : 0) | ((prm->flags & RT_FLAG_OPEN_INTERVAL) ? rtk::kVarOpen : 0) |
                 ((prm->flags & RT_FLAG_METAL_UNIT_VECTOR) ? rtk::kVarMetalUnit : 0) |
                 ((prm->flags & RT_FLAG_ACCEL_BVH) ? rtk::kVarBvh : 0) |
                 ((prm->flags & RT_FLAG_COUNT_WORK) ? rtk::kVarStats : 0) |
@@ -490,9 +528,10 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
   const long long units = lp.units, ranges = lp.ranges, chunks = lp.chunks, entries = lp.entries;
   const long long launches = ranges * chunks;
   kp.units = (int)units;
-  const int f = sum_bits(prm->spp);
+  const int f = fmt.f;
   kp.qscale = std::ldexp(1.0f, f);
   kp.qinv = std::ldexp(1.0f, -f);
+  kp.vcap = fmt.vcap;
   // F < 20 (spp >= 4096): truncation would bias a dark pixel by up to 2^-F per
   // sample (0.03 level at F = 20); stochastic rounding is unbiased for every
   // spp
@@ -551,7 +590,21 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
   // several units or launches per tile add their integer sums into the
   // zeroed frame (after the pilot, which renders into it too); finish_sums
   // converts them
-  if (kp.sum_atomic) RT_HIP(hipMemsetAsync(accum_rgb, 0, frame_floats * sizeof(float), st));
+  if (kp.sum_atomic && fmt.wide) {
+    // 64-bit sums do not fit the caller's fp32 frame: a scratch frame of the
+    // context's (renders of one context are serialised), converted at the end
+    if (c->wide_n < frame_floats) {
+      (void)hipFree(c->d_wide);
+      c->d_wide = nullptr;
+      c->wide_n = 0;
+      RT_HIP(hipMalloc(&c->d_wide, frame_floats * sizeof(uint64_t)));
+      c->wide_n = frame_floats;
+    }
+    RT_HIP(hipMemsetAsync(c->d_wide, 0, frame_floats * sizeof(uint64_t), st));
+    kp.out = reinterpret_cast<float *>(c->d_wide);
+  } else if (kp.sum_atomic) {
+    RT_HIP(hipMemsetAsync(accum_rgb, 0, frame_floats * sizeof(float), st));
+  }
   {
     while (c->ev_launch.size() < (size_t)launches) {
       hipEvent_t ev = nullptr;
@@ -578,7 +631,10 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
   }
   c->last_launches += (uint32_t)launches;
   c->enq_launches = (uint32_t)launches;
-  if (kp.sum_atomic) RT_HIP(rtk::launch_finish_sums(reinterpret_cast<uint32_t *>(accum_rgb), frame_floats, kp.qinv, st));
+  if (kp.sum_atomic && fmt.wide)
+    RT_HIP(rtk::launch_finish_sums_wide(c->d_wide, accum_rgb, frame_floats, kp.qinv, st));
+  else if (kp.sum_atomic)
+    RT_HIP(rtk::launch_finish_sums(reinterpret_cast<uint32_t *>(accum_rgb), frame_floats, kp.qinv, st));
   RT_HIP(hipEventRecord(c->ev_done, st));
   c->last_stream = st;
   c->have_done = true;
@@ -701,6 +757,7 @@ int rt_internal_accel_info(const rt_scene_view *s, int grid_placement, double gr
     return RT_ERR_INVALID;
   static const int kMap[4] = {-1, rtk::kGridLds, rtk::kGridCells, rtk::kGridGlobal};
   rtk::accel_options o;
+  o.wide = rtk::max_albedo(s) > 1.0;
   o.grid_placement = kMap[grid_placement];
   o.grid_scale = grid_scale == 0.0 ? 1.0 : grid_scale;
   rtk::accel_build a;
@@ -741,6 +798,14 @@ int rt_internal_accel_info(const rt_scene_view *s, int grid_placement, double gr
   v[16] = cells ? kPlaceOut[a.grid_placement] : 0u;
   v[17] = (uint64_t)std::llround(a.grid_scale * 1000.0);
   std::memcpy(out, v, std::min<size_t>(n_out, RT_ACCEL_INFO_N) * sizeof(uint64_t));
+  return RT_OK;
+}
+
+int rt_internal_sealed(const rt_scene_view *s, uint8_t *out, size_t n_out) {
+  if (!rtk::scene_ok(s) || (n_out && !out)) return RT_ERR_INVALID;
+  std::vector<uint8_t> v;
+  rtk::sealed_spheres(s, v);
+  if (n_out && !v.empty()) std::memcpy(out, v.data(), std::min<size_t>(n_out, v.size()));
   return RT_OK;
 }
 

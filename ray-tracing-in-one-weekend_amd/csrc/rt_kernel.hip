@@ -34,6 +34,7 @@
 #include <array>
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 #include <utility>
 
 #include "rt.h"
@@ -782,8 +783,12 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
 // the kernarg segment where they are used (kernargs(), as_const()) instead of
 // being held in SGPRs for the whole kernel: 94 SGPRs + 21 spilled -> 69 at 7
 // waves.
-template <bool OPEN, bool METAL_UNIT, bool BVH, bool STATS, bool GRID, int GP>
+// WIDE (scenes with an albedo above 1, rt_scene_upload): 64-bit pixel sums
+//  and the radiance clamps below; the default build's
+// code and registers are untouched.
+template <bool OPEN, bool METAL_UNIT, bool BVH, bool STATS, bool GRID, int GP, bool WIDE>
 __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
+  typedef typename std::conditional<WIDE, unsigned long long, uint32_t>::type sum_t;
   // Per-lane values that the bounce loop rarely needs are not kept live (VGPR
   // pressure at 8 waves): the wave keeps its tile origin (col0, lrow0, SGPRs),
   // the lane its current pixel slot, sample and global pixel index; column and
@@ -803,7 +808,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   // the tile has samples left; a pixel's sum is an exact integer, whichever
   // lanes traced its samples in whatever order.
   const uint32_t kend = (s_end > s_begin ? s_end - s_begin : 0u) << 6;
-  __shared__ uint32_t s_sum[3][kBlock];                 // the tiles' fixed-point pixel sums
+  __shared__ sum_t s_sum[3][kBlock];                    // the tiles' fixed-point pixel sums
   __shared__ uint32_t s_rowpix[kWavesPerBlock][kTile];  // global pixel index of (x = 0, y)
   bool own_valid;
   {
@@ -899,10 +904,16 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         const float a = 0.5f * (dy + 1.0f);
         const float s0 = 1.0f - a;
         const int i = wave * 64 + (int)slot;
-        const float xr = thr * fmaf(a, 0.5f, s0) * q.qscale;
-        const float xg = thg * fmaf(a, 0.7f, s0) * q.qscale;
-        const float xb = thb * (s0 + a) * q.qscale;
-        uint32_t nr = (uint32_t)xr, ng = (uint32_t)xg, nb = (uint32_t)xb;
+        float xr = thr * fmaf(a, 0.5f, s0), xg = thg * fmaf(a, 0.7f, s0), xb = thb * (s0 + a);
+        if (WIDE) {  // radiance above the format's bound is clamped (v <= vcap, rt_api.cpp sum_format)
+          xr = fminf(xr, q.vcap);
+          xg = fminf(xg, q.vcap);
+          xb = fminf(xb, q.vcap);
+        }
+        xr *= q.qscale;
+        xg *= q.qscale;
+        xb *= q.qscale;
+        sum_t nr = (sum_t)xr, ng = (sum_t)xg, nb = (sum_t)xb;
         if (q.dither) {  // spp >= 4096: stochastic rounding
           const float u = dither_u(pix, sample, q.seed32);
           nr += __builtin_amdgcn_fractf(xr) > u ? 1u : 0u;
@@ -966,16 +977,20 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         float rx, ry, rz;
         reflect3(dx, dy, dz, nx, ny, nz, dn, rx, ry, rz);
         float sx, sy, sz;
-        // An opaque sphere hit from inside: the path got
-        // in past the surface within t_min of a contact point (a glass sphere
-        // resting on the ground: src/cpu does the same, main.cc:19) and can
-        // never leave -- every lambertian or metal scatter off an inner wall
-        // points inward -- so it ends black here, as it would at the depth cap,
-        // without tracing the rest inside (segments of up to 2000 units from
-        // origins beyond the grid's padding bound, each a whole-scene scan:
-        // C4's rank share 408 -> 143 ms at 100 spp, profiles/r03d_c4_ab.log)
-        bool scattered = front;
+        bool scattered = true;
         if (sr.kind == RT_LAMBERTIAN) {
+          // The opaque-inside rule: a sealed lambertian
+          // sphere (no other ball overlaps its ball, rt_accel.cpp
+          // sealed_spheres) hit at its exiting root -- the ray started inside
+          // its ball, having got in past the surface within t_min of a contact
+          // point (a glass sphere resting on the ground) -- ends the path black.
+          // In the reference's arithmetic such a path hits the same sphere at
+          // t = |r| after every scatter (its chords are n + u long) until the
+          // depth cap; here it ends at once, without segments of up to 2000
+          // units from origins beyond the grid's padding bound (C4's rank share
+          // 408 -> 143 ms at 100 spp, profiles/r03d_c4_ab.log).  Keyed on the
+          // root (near), not the face: a negative radius flips the face only.
+          scattered = near || !sr.sealed;
           // material.h:19-30
           sx = nx + ux;
           sy = ny + uy;
@@ -993,14 +1008,13 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           sx = fmaf(fz, ux, rx);
           sy = fmaf(fz, uy, ry);
           sz = fmaf(fz, uz, rz);
-          scattered = scattered && dot3(sx, sy, sz, nx, ny, nz) > 0.0f;
+          scattered = dot3(sx, sy, sz, nx, ny, nz) > 0.0f;
         } else {
           // dielectric, material.h:57-87 (r0 is the same for ior and 1/ior)
           const float ratio = front ? sr.inv_param : sr.param;
           const float cos_t = fminf(-dn, 1.0f);
           // ratio sin > 1 (material.h:64), squared: no square root
           const bool cannot = (ratio * ratio) * fmaf(-cos_t, cos_t, 1.0f) > 1.0f;
-          scattered = true;  // a dielectric is entered and left
           if (cannot || schlick(cos_t, sr.r0) > unif(r.x)) {
             sx = rx;
             sy = ry;
@@ -1013,6 +1027,11 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         thr *= sr.ar;
         thg *= sr.ag;
         thb *= sr.ab;
+        if (WIDE) {  // albedos above 1: the throughput stays finite (inf x 0 would be NaN)
+          thr = fminf(thr, 0x1p100f);
+          thg = fminf(thg, 0x1p100f);
+          thb = fminf(thb, 0x1p100f);
+        }
         ++depth;
         if (!scattered || depth >= q.max_depth) {
           path_done = true;  // absorbed, or bounce limit (main.cc:16-17): black
@@ -1056,7 +1075,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         out[1] = (float)s_sum[1][i] * q.qinv;
         out[2] = (float)s_sum[2][i] * q.qinv;
       } else {  // the tile's units / launches add their integer sums (finish_sums converts)
-        uint32_t *acc = reinterpret_cast<uint32_t *>(q.out) + o;
+        sum_t *acc = reinterpret_cast<sum_t *>(q.out) + o;  // WIDE: the context's 64-bit scratch frame
         atomicAdd(acc + 0, s_sum[0][i]);
         atomicAdd(acc + 1, s_sum[1][i]);
         atomicAdd(acc + 2, s_sum[2][i]);
@@ -1105,6 +1124,14 @@ __global__ __launch_bounds__(256) void finish_sums(uint32_t *__restrict__ frame,
   // every access goes through the uint32 view: the float result is stored as its bits
   for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < n; j += (uint64_t)gridDim.x * 256u)
     frame[j] = __float_as_uint((float)frame[j] * qinv);
+}
+
+// The same for WIDE renders: the 64-bit sums live in the context's scratch
+// frame (the caller's fp32 frame has 4 bytes per channel), converted into it.
+__global__ __launch_bounds__(256) void finish_sums_wide(const uint64_t *__restrict__ sums, float *__restrict__ frame,
+                                                        uint64_t n, float qinv) {
+  for (uint64_t j = (uint64_t)blockIdx.x * 256u + threadIdx.x; j < n; j += (uint64_t)gridDim.x * 256u)
+    frame[j] = (float)sums[j] * qinv;
 }
 
 // Known-answer evaluation of the render kernel's own device arithmetic
@@ -1234,16 +1261,16 @@ __global__ __launch_bounds__(256) void tonemap_kernel(const float *__restrict__ 
 template <int V>
 void launch_variant(unsigned blocks, size_t lds, hipStream_t st, const kparams &kp) {
   constexpr bool O = V & kVarOpen, U = V & kVarMetalUnit, B = V & kVarBvh, S = V & kVarStats;
-  constexpr bool G = B && (V & kVarGrid);
+  constexpr bool G = B && (V & kVarGrid), W = V & kVarWide;
   constexpr int P = G ? ((V >> kVarPlaceShift) & 3) % 3 : kGridGlobal;
-  render_kernel<O, U, B, S, G, P><<<blocks, kBlock, G ? lds : 0, st>>>(kp);
+  render_kernel<O, U, B, S, G, P, W><<<blocks, kBlock, G ? lds : 0, st>>>(kp);
 }
 using launch_fn = void (*)(unsigned, size_t, hipStream_t, const kparams &);
 template <int... V>
 constexpr auto launch_table(std::integer_sequence<int, V...>) {
   return std::array<launch_fn, sizeof...(V)>{&launch_variant<V>...};
 }
-constexpr auto kLaunch = launch_table(std::make_integer_sequence<int, 4 << kVarPlaceShift>{});
+constexpr auto kLaunch = launch_table(std::make_integer_sequence<int, 2 * kVarWide>{});
 
 hipError_t launch_render(int variant, unsigned blocks, size_t lds_bytes, hipStream_t st, const kparams &kp) {
   if (variant < 0 || variant >= (int)kLaunch.size()) return hipErrorInvalidValue;
@@ -1254,6 +1281,12 @@ hipError_t launch_render(int variant, unsigned blocks, size_t lds_bytes, hipStre
 hipError_t launch_finish_sums(uint32_t *frame, uint64_t n, float qinv, hipStream_t st) {
   const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, 256u * 64u);
   finish_sums<<<grid, 256, 0, st>>>(frame, n, qinv);
+  return hipGetLastError();
+}
+
+hipError_t launch_finish_sums_wide(const uint64_t *sums, float *frame, uint64_t n, float qinv, hipStream_t st) {
+  const unsigned grid = (unsigned)std::min<uint64_t>((n + 255) / 256, 256u * 64u);
+  finish_sums_wide<<<grid, 256, 0, st>>>(sums, frame, n, qinv);
   return hipGetLastError();
 }
 

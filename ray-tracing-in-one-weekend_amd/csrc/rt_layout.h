@@ -90,7 +90,8 @@ struct __attribute__((aligned(16))) shade_rec {
   float radius, ks;
   float inv_param;          // 1/ior (dielectric)
   float r0;                 // Schlick r0 = ((1-ior)/(1+ior))^2 (dielectric)
-  float pad0, pad1, pad2;
+  uint32_t sealed;          // 1: a lambertian ball no other ball overlaps (rt_accel.cpp sealed_spheres)
+  float pad1, pad2;
 };
 
 // Where the layer grid lives during a launch (rt_context_set_option
@@ -135,7 +136,10 @@ struct kparams {
   // stochastically (unbiased for every spp)
   float qscale, qinv;  // 2^F, 2^-F
   int dither, block_base;
-  int block_stride, pad_b;
+  int block_stride;
+  // WIDE renders (a scene albedo above 1): 64-bit sums, a sample's radiance
+  // clamped at vcap (rt_api.cpp sum_format)
+  float vcap;
   // device buffers (rt_context; out = the caller's frame tile)
   const struct pair_geom *scan_geom;  // brute-force order
   const struct pair_geom *geom;       // BVH leaf order
@@ -174,6 +178,8 @@ __host__ __device__ constexpr size_t grid_lds_bytes(int placement, long long n_i
 // blocks (8 waves per SIMD) still fit in the CU's 160 KB
 constexpr size_t kStaticLds = 3 * kBlock * 4 + kWavesPerBlock * kTile * 4;
 constexpr size_t kGridLdsMax = 160 * 1024 / 8 - kStaticLds;
+// WIDE builds hold 64-bit pixel sums: 3 KB more static LDS
+constexpr size_t kGridLdsMaxWide = kGridLdsMax - 3 * kBlock * 4;
 
 // ---- launch interface (defined in rt_kernel.hip) ----
 // render_kernel variant bits
@@ -183,10 +189,12 @@ enum {
   kVarBvh = 4,        // RT_FLAG_ACCEL_BVH
   kVarStats = 8,      // RT_FLAG_COUNT_WORK (and the pilot)
   kVarGrid = 16,      // the layer-grid walk (with kVarBvh on a layer scene)
-  kVarPlaceShift = 5  // bits 5-6: the grid placement (kGridGlobal / kGridLds / kGridCells)
+  kVarPlaceShift = 5, // bits 5-6: the grid placement (kGridGlobal / kGridLds / kGridCells)
+  kVarWide = 128      // 64-bit pixel sums (a scene albedo above 1)
 };
 hipError_t launch_render(int variant, unsigned blocks, size_t lds_bytes, hipStream_t st, const kparams &kp);
 hipError_t launch_finish_sums(uint32_t *frame, uint64_t n, float qinv, hipStream_t st);
+hipError_t launch_finish_sums_wide(const uint64_t *sums, float *frame, uint64_t n, float qinv, hipStream_t st);
 hipError_t launch_tonemap(bool fp32, const float *sums, uint64_t n, int spp, const void *thresholds,
                           uint8_t *out, hipStream_t st);
 hipError_t launch_kat(int kind, const double *in, int n, double *out);

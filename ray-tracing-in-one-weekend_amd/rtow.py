@@ -145,6 +145,8 @@ def lib():
         if hasattr(L, "rt_internal_launch_plan"):
             L.rt_internal_launch_plan.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_void_p,
                                                   ctypes.c_size_t]
+        if hasattr(L, "rt_internal_sealed"):
+            L.rt_internal_sealed.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
         if hasattr(L, "rt_context_set_option"):  # (absent in pre-ABI-4 builds loaded for A/B runs)
             L.rt_context_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
         _lib = L
@@ -411,6 +413,16 @@ def accel_info(scene, grid_mode="auto", grid_scale=0.0):
     check(lib().rt_internal_accel_info(ctypes.byref(v), GRID_PLACEMENTS[grid_mode], float(grid_scale),
                                        out.ctypes.data, out.size), "rt_internal_accel_info")
     return {k: int(x) for k, x in zip(ACCEL_INFO_KEYS, out)}
+
+
+def sealed(scene):
+    """Per sphere, whether the kernel's opaque-inside rule applies to it (a
+    sealed lambertian sphere), computed on the host
+    (rt_internal_sealed; no device): a bool array."""
+    v = scene.view()
+    out = np.zeros(max(scene.n, 1), np.uint8)
+    check(lib().rt_internal_sealed(ctypes.byref(v), out.ctypes.data, scene.n), "rt_internal_sealed")
+    return out[:scene.n].astype(bool)
 
 
 LAUNCH_PLAN_KEYS = ("ranges", "chunks", "units", "entries", "launches")

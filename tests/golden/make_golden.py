@@ -19,6 +19,10 @@ oracle/_ref/ref_harness from the reference's own src/cpu sources
   ref_tenk_160x90x16(.|_shift).ppm.gz  the 10 000-sphere stress scene
                              (rt_scene_final(50), dumped to a temp file and
                              rendered by the reference's own classes)
+  ref_embed(|_shift)_320x180x256.ppm.gz  a glass sphere half-embedded in a
+                             lambertian sphere (tests/fixture_scenes.py)
+  ref_negop(|_shift)_320x180x256.ppm.gz  lambertian and metal spheres of
+                             negative radius (tests/fixture_scenes.py)
   ref_stats.json             segments / sphere tests / seconds per render + SHA-256
   kat.jsonl                  known-answer vectors: camera basis, sphere::hit,
                              reflect, refract, reflectance, write_color
@@ -86,6 +90,17 @@ def main():
         "ref_tenk_160x90x16": ["render", "160", "16", "9", "16", "50", "file:" + tenk, "0"],
         "ref_tenk_shift_160x90x16": ["render", "160", "16", "9", "16", "50", "file:" + tenk, shift],
     }
+    # the opaque-inside rule's fixtures (tests/fixture_scenes.py): exact float32 dumps
+    sys.path.insert(0, os.path.dirname(HERE))
+    import fixture_scenes
+    from random_scenes import dump_scene_exact
+    w, h, spp = fixture_scenes.FIXTURE_SIZE
+    for key, make in fixture_scenes.FIXTURES.items():
+        path = os.path.join(tmp, key + ".txt")
+        dump_scene_exact(make(rtow), path)
+        for tag, skip in (("", "0"), ("_shift", shift)):
+            renders["ref_%s%s_%dx%dx%d" % (key, tag, w, h, spp)] = [
+                "render", str(w), "16", "9", str(spp), "50", "file:" + path, skip]
     if a.only is not None:
         renders = {k: v for k, v in renders.items() if k in a.only}
     stats_path = os.path.join(HERE, "ref_stats.json")
@@ -101,7 +116,9 @@ def main():
         st = json.loads(r.stderr.decode().strip().splitlines()[-1])
         st["sha256"] = hashlib.sha256(ppm).hexdigest()
         st["bytes"] = len(ppm)
-        st["args"] = [x if not x.startswith("file:") else "file:<rt_scene_final(50) dump>" for x in args]
+        st["args"] = [x if not x.startswith("file:") else
+                      "file:<%s dump>" % os.path.basename(x[5:]).replace("tenk.txt", "rt_scene_final(50)")
+                      for x in args]
         with gzip.GzipFile(os.path.join(HERE, name + ".ppm.gz"), "wb", mtime=0) as g:
             g.write(ppm)
         print(name, st, flush=True)

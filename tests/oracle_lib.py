@@ -190,3 +190,14 @@ def sample_probe(kind, n, seed=1):
     out = np.zeros((n, 3), np.float32)
     assert L.rto_sample_probe(kind, n, seed, out.ctypes.data) == 0
     return out
+
+
+def sealed(scene):
+    """The oracle's sealed spheres (the kernel specification's opaque-inside
+    rule): a bool array, one per sphere."""
+    v = scene.view()
+    out = np.zeros(max(scene.n, 1), np.uint8)
+    L = lib()
+    L.rto_sealed.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    assert L.rto_sealed(ctypes.addressof(v), out.ctypes.data) == 0
+    return out[:scene.n].astype(bool)

@@ -72,3 +72,31 @@ def test_committed_summaries_name_their_share():
         w = int(d.get("world", 1))
         assert path.endswith(".json" if w == 1 else f"_w{w}.json"), path
         assert d["workload"] == WORKLOAD
+
+
+def test_counters_of_other_device_code_are_nulled():
+    """A summary collected on other kernel code: the line names it and says
+    so, and every counter-derived field is null (Weak 4)."""
+    for world in (1, 2, 4, 8):
+        pmc, reason = bench.load_pmc(WORKLOAD, "bvh", world)
+        if not pmc:
+            continue
+        roof = bench.roofline(WORK, pmc["kernel_s_pmc_pass"], "bvh", pmc, None, "f" * 16)
+        assert roof["pmc_matches_device_code"] is False
+        assert roof["pmc_source"] and roof["pmc_source"] in roof["pmc_null_reason"]
+        assert "f" * 16 in roof["pmc_null_reason"]
+        assert roof["valu_issue"] is None and roof["valu_lane_util"] is None
+        assert roof["hbm"] is None and roof["traffic"] is None
+        assert 0 < roof["frac"] <= 1  # from the live HIP-event time and the work counters
+
+
+def test_committed_summaries_carry_the_built_device_code(rtow):
+    """Every committed pmc_traffic_bvh*.json (the N = 1, 2, 4, 8 lines' counter
+    sources) was collected on the kernel this tree builds: the sha256 of the
+    library's device code matches (tools/profile_round.sh,
+    tools/profile_shares.sh re-collect them after a kernel change)."""
+    sha = rtow.device_code_sha16()
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_traffic_bvh*.json")))
+    assert len(paths) == 4
+    for path in paths:
+        assert json.load(open(path))["device_code_sha16"] == sha, os.path.basename(path)

@@ -220,11 +220,13 @@ def test_lds_resident_grid_equals_global_grid(rtow, gpu_ctx):
 
 
 @pytest.mark.gpu
-def test_scene_upload_rejects_albedo_outside_unit_interval(rtow):
-    """The fixed-point pixel sums need a sample's radiance
-    <= 1: rt_scene_upload refuses a lambertian or metal albedo outside [0, 1]
-    (or NaN) with RT_ERR_INVALID and keeps the previous scene; a dielectric's
-    albedo is ignored, as the kernel ignores it."""
+def test_scene_upload_albedo_domain(rtow):
+    """rt_scene_upload takes every finite albedo >= 0 (the reference's
+    constructors take any colour, src/cpu/material.h:17,38; above 1 the render
+    uses 64-bit pixel sums) and refuses a negative or
+    non-finite lambertian / metal albedo with RT_ERR_INVALID, keeping the
+    previous scene; a dielectric's albedo is ignored, as the kernel ignores
+    it.  An albedo of exactly 1 keeps the 32-bit format (same bits as before)."""
     import dataclasses
     base = rtow.final_scene()
     with rtow.Context(0) as ctx:
@@ -234,7 +236,7 @@ def test_scene_upload_rejects_albedo_outside_unit_interval(rtow):
         before, _ = ctx.render(cam, prm)
         lam = int(np.nonzero(base.kind == rtow.RT_LAMBERTIAN)[0][0])
         die = int(np.nonzero(base.kind == rtow.RT_DIELECTRIC)[0][0])
-        for bad in (1.0001, -1e-7, float("nan")):
+        for bad in (-1e-7, float("nan"), float("inf")):
             alb = base.albedo.copy()
             alb[lam, 1] = bad
             with pytest.raises(rtow.RTError) as ei:
@@ -247,6 +249,15 @@ def test_scene_upload_rejects_albedo_outside_unit_interval(rtow):
         ctx.upload(dataclasses.replace(base, albedo=alb))
         same, _ = ctx.render(cam, prm)
         assert np.array_equal(before, same)
+        for hot in (1.0001, 3.0, 1e30):  # accepted: bit-exact vs the oracle
+            alb = base.albedo.copy()
+            alb[lam] = hot
+            sc = dataclasses.replace(base, albedo=alb)
+            ctx.upload(sc)
+            got, st = ctx.render(cam, prm)
+            want, segs = kernel_render(sc, cam, prm)
+            assert np.array_equal(got, want) and st.segments == segs, hot
+            assert np.isfinite(got).all()
 
 
 # ---- round 3: the configs at their own sample counts, the sum format's

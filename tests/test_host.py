@@ -203,7 +203,7 @@ def test_ppm_writer_p3_and_p6(rtow, tmp_path):
 def test_abi_exports_every_declared_symbol(rtow):
     hdr = open(os.path.join(ROOT, "include", "rt.h")).read()
     names = sorted(set(re.findall(r"^\s*(?:[\w\*\s]+?)\b(rt_\w+)\s*\(", hdr, re.M)))
-    assert len(names) == 24, names
+    assert len(names) == 25, names
     L = rtow.lib()
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
@@ -353,7 +353,8 @@ def test_host_code_under_asan_ubsan():
 def test_scene_validation_on_host(rtow):
     """rt_scene_upload's validation (shared with rt_internal_accel_info, so it
     runs without a device): non-finite centres, zero radii, unknown materials
-    and lambertian / metal albedos outside [0, 1] are RT_ERR_INVALID; a
+    and negative or non-finite lambertian / metal albedos are RT_ERR_INVALID;
+    albedos above 1 are accepted (64-bit pixel sums); a
     dielectric's albedo is ignored."""
     import dataclasses
     base = rtow.final_scene()
@@ -371,13 +372,20 @@ def test_scene_validation_on_host(rtow):
         return dataclasses.replace(base, **{name: a})
 
     bad = [with_("cx", 5, float("nan")), with_("cz", 5, float("inf")), with_("radius", 5, 0.0),
-           with_("kind", 5, 7), with_("albedo", lam, 1.5, 0), with_("albedo", met, -0.1, 2),
-           with_("albedo", lam, float("nan"), 1)]
+           with_("kind", 5, 7), with_("albedo", met, -0.1, 2), with_("albedo", lam, float("nan"), 1),
+           with_("albedo", lam, float("inf"), 2)]
     for sc in bad:
         with pytest.raises(rtow.RTError) as ei:
             rtow.accel_info(sc)
         assert ei.value.status == rtow.RT_ERR_INVALID
     assert rtow.accel_info(with_("albedo", die, 9.0, 0))["layer_mode"] == 1
+    # energy-creating albedos (the reference's constructors take any colour):
+    # accepted; with 3 KB more static LDS for the 64-bit sums the final
+    # scene's grid keeps only its cells in LDS
+    hot = with_("albedo", lam, 1.5, 0)
+    assert rtow.accel_info(hot)["layer_mode"] == 1
+    assert rtow.accel_info(hot)["grid_placement"] == rtow.RT_GRID_CELLS_LDS
+    assert rtow.accel_info(base)["grid_placement"] == rtow.RT_GRID_LDS
 
 
 def test_turn_table_deterministic_and_accurate(tmp_path):
@@ -418,3 +426,55 @@ def test_turn_table_deterministic_and_accurate(tmp_path):
     exact = np.stack([np.cos(a), np.sin(a)], axis=1)
     ulp = np.spacing(np.abs(exact).astype(np.float32)).astype(np.float64)
     assert np.all(np.abs(got.astype(np.float64) - exact) <= np.maximum(ulp, 1e-15))  # exact zeros where cos / sin vanish
+
+
+def test_sealed_spheres_product_equals_oracle(rtow, oracle):
+    """The opaque-inside rule applies to sealed spheres only (DESIGN.md 2 step
+    4): lambertian, |r| > 2 t_min, no other ball overlapping its ball.  The
+    product's sweep (rt_internal_sealed) equals the oracle's brute-force
+    restatement on the final scene, C4's 10 000 spheres, the five-sphere
+    scene, the rule's reference fixtures and 24 random scenes with
+    overlapping and nested spheres."""
+    import fixture_scenes
+    import random_scenes
+    scenes = {"final": rtow.final_scene(), "c4": rtow.final_scene(half_extent=50), "five": rtow.five_scene()}
+    scenes.update({k: f(rtow) for k, f in fixture_scenes.FIXTURES.items()})
+    scenes.update({"free%d" % k: random_scenes.free_scene(rtow, k) for k in range(24)})
+    for name, s in scenes.items():
+        a, b = rtow.sealed(s), oracle.sealed(s)
+        assert np.array_equal(a, b), name
+        assert not a[s.kind != 0].any(), name  # metal and glass are never sealed
+    final, c4 = scenes["final"], scenes["c4"]
+    # the ground is sealed (the big glass sphere touches it at one point,
+    # |C_a - C_b| = 1001 = r_a + r_b exactly); the big lambertian sphere at
+    # (-4, 1, 0) is overlapped by small spheres
+    for s in (final, c4):
+        assert s.radius[0] == 1000 and rtow.sealed(s)[0]
+        big = np.flatnonzero((s.radius == 1) & (s.kind == 0))
+        assert len(big) == 1 and not rtow.sealed(s)[big[0]]
+    assert rtow.sealed(final).sum() == 347 and (final.kind == 0).sum() == 382
+    emb = scenes["embed"]
+    assert rtow.sealed(emb).tolist() == [True, False, False]  # the glass overlaps the r = 1 ball
+    assert rtow.sealed(scenes["negop"]).tolist() == [True, True, False]  # |r| counts
+    # five: the ground (r = 100) touches nothing; the centre sphere is sealed
+    assert rtow.sealed(scenes["five"]).tolist() == [True, True, False, False, False]
+
+
+def test_sealed_touching_and_tiny_spheres(rtow, oracle):
+    """Touching at one point keeps both balls sealed; any overlap unseals
+    both; a lambertian ball of |r| <= 2 t_min is never sealed."""
+    f32 = np.float32
+
+    def mk(rows):
+        a = np.array(rows, np.float64)
+        return rtow.Scene(a[:, 0].astype(f32), a[:, 1].astype(f32), a[:, 2].astype(f32), a[:, 3].astype(f32),
+                          np.zeros(len(rows), np.uint32), np.full((len(rows), 3), 0.5, f32),
+                          np.zeros(len(rows), f32))
+    touching = mk([(0, 0, 0, 1), (3, 0, 0, 2), (0, 0.5, 0, 0.0015), (9, 9, 9, 0.003)])
+    assert rtow.sealed(touching).tolist() == [False, True, False, True]  # (0, .5, 0) lies inside ball 0
+    apart = mk([(0, 0, 0, 1), (3, 0, 0, 2), (9, 9, 9, 0.0019)])
+    assert rtow.sealed(apart).tolist() == [True, True, False]
+    overlap = mk([(0, 0, 0, 1), (2.999, 0, 0, 2)])
+    assert rtow.sealed(overlap).tolist() == [False, False]
+    for s in (touching, apart, overlap):
+        assert np.array_equal(rtow.sealed(s), oracle.sealed(s))

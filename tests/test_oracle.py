@@ -439,3 +439,21 @@ def test_image23_brightness_is_src_gpu_fp32_hit_arithmetic(rtow):
     assert np.all(np.abs(bias) <= 0.05), report
     assert err <= 1.15 * floor, report
     assert np.all((explained >= 0.12) & (explained <= 0.25)), report
+
+
+@pytest.mark.parametrize("key", ["embed", "negop", "hot"])
+def test_rule_and_albedo_fixtures_vs_reference(rtow, key):
+    """The opaque-inside rule against the reference's own
+    src/cpu on the rule's fixtures (tests/fixture_scenes.py, 320x180 @ 256
+    spp, two seeds): a glass sphere half-embedded in a lambertian sphere --
+    the lambertian ball is overlapped, so the rule does not apply and paths
+    inside it go on as in the reference -- and lambertian / metal spheres of
+    negative radius, which the round-3 rule (keyed on the face, not the root)
+    rendered black: bias -12.7 levels, 10.6 % fewer segments.  "hot": albedos
+    above 1 (64-bit pixel sums, radiance clamp)."""
+    import fixture_scenes
+    scene = fixture_scenes.FIXTURES[key](rtow)
+    w, h, spp = fixture_scenes.FIXTURE_SIZE
+    cam = rtow.camera_cpu(aspect=16.0 / 9.0)
+    runs = [kernel_render(scene, cam, rtow.make_params(w, h, spp, seed=seed)) for seed in (1, 2)]
+    fixture_scenes.p2_check(rtow, key, [s for s, _ in runs], [n for _, n in runs])

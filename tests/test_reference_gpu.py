@@ -360,3 +360,30 @@ def test_device_reflect_refract_reflectance_random_kat(rtow, gpu_ctx):
     print("worst reflect", e_rf, "refract", e_rr, "reflectance", e_sc)
     # measured: 1.5e-7, 4.5e-7, 1.7e-7 (profiles/r03ag_vector_kat.log)
     assert e_rf <= 1e-6 and e_rr <= 2e-6 and e_sc <= 1e-6, (e_rf, e_rr, e_sc)
+
+
+@pytest.mark.parametrize("key", ["embed", "negop", "hot"])
+def test_rule_and_albedo_fixtures_vs_reference(rtow, gpu_ctx, key):
+    """The opaque-inside rule's reference fixtures (tests/fixture_scenes.py,
+    src/cpu through ref_harness file:, 320x180 @ 256 spp): a glass sphere
+    half-embedded in a lambertian sphere (not sealed: paths inside it go on
+    and may leave through the glass) and lambertian / metal spheres of
+    negative radius (lit, not black); "hot": albedos above 1 (64-bit pixel
+    sums).  The product through the C ABI, two
+    seeds, each bit-exact vs the oracle; P2 bounds in fixture_scenes.p2_check."""
+    import fixture_scenes
+    scene = fixture_scenes.FIXTURES[key](rtow)
+    w, h, spp = fixture_scenes.FIXTURE_SIZE
+    cam = rtow.camera_cpu(aspect=16.0 / 9.0)
+    gpu_ctx.upload(scene)
+    sums, segs = [], []
+    for seed in (1, 2):
+        p = rtow.make_params(w, h, spp, seed=seed, flags=GRID)
+        got, st = gpu_ctx.render(cam, p)
+        want, n = kernel_render(scene, cam, p)
+        assert np.array_equal(got, want) and st.segments == n, (seed, int((got != want).sum()))
+        img = device_tonemap(rtow, gpu_ctx, got, spp)
+        assert np.array_equal(img, rtow.tonemap(got, spp))
+        sums.append(got)
+        segs.append(st.segments)
+    fixture_scenes.p2_check(rtow, key, sums, segs)
