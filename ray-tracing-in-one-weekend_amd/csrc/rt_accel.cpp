@@ -394,6 +394,13 @@ struct bvh_builder {
     std::vector<uint32_t> in, out;
     for (uint32_t i = 0; i < n; ++i) (key[i] == key[best] ? in : out).push_back(i);
     if (out.size() > kMaxExtra) return n;
+    // the largest extra first: the grid build's extras scan runs slot 0's root
+    // sequence on its own and compacts the others' (rt_kernel.hip scan_extras);
+    // the ground, a candidate for almost every line, belongs there.  The
+    // closest hit does not depend on the order (ties go by original index).
+    std::stable_sort(out.begin(), out.end(), [&](uint32_t a, uint32_t b) {
+      return std::fabs((double)s->radius[a]) > std::fabs((double)s->radius[b]);
+    });
     layer_mode = true;
     layer_cy = key[best].first;
     std::copy(in.begin(), in.end(), ord.begin());

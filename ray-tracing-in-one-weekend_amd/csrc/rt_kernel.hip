@@ -268,6 +268,9 @@ __device__ __forceinline__ void camera_dir(const kparams &p, const uint4 r, floa
   oy = p.cam.eye[1];
   oz = p.cam.eye[2];
   if (p.cam.has_lens) {
+    // a real (wave-uniform) branch: without the barrier the compiler computes
+    // the lens origin for every camera and selects (9 VALU per new path)
+    asm volatile("" ::: "memory");
     ox = fmaf(ddy, p.cam.lens_v[0], fmaf(ddx, p.cam.lens_u[0], ox));
     oy = fmaf(ddy, p.cam.lens_v[1], fmaf(ddx, p.cam.lens_u[1], oy));
     oz = fmaf(ddy, p.cam.lens_v[2], fmaf(ddx, p.cam.lens_u[2], oz));
@@ -401,46 +404,72 @@ __device__ __forceinline__ void scan_pairs(const RT_CONST pair_geom *__restrict_
   }
 }
 
-// scan_pairs in plain fp32, one sphere at a time: the same fma per sphere as
-// one half of the packed form (the same bits), without splatting the ray terms
-// into VGPR pairs and without moving the second SGPR operand of every
-// v_pk_fma_f32 into a VGPR first (the grid build's extras: 4 spheres a step)
-template <bool OPEN, int NP, bool STATS>
-__device__ __forceinline__ void scan_pairs_scalar(const RT_CONST pair_geom *__restrict__ g, int slot0,
-                                                  const RT_CONST int *__restrict__ orig, const ray_pre &r,
-                                                  hit_state &hs, uint32_t &roots) {
-  float h[2 * NP], e[2 * NP], ks[2 * NP];
-  bool c[2 * NP];
-  uint64_t any = 0;
+// The extras of the grid build (the spheres off the layer: in the final scene
+// the ground and the three big spheres), four per group, with their candidates'
+// root sequences compacted: a lane's candidates among spheres J0..3 run one
+// per round, the lowest remaining slot first, so a round runs for every lane
+// that still has one and the wave runs as many rounds as its busiest lane has
+// candidates (usually one: a line seldom meets two of the big spheres),
+// instead of one sequence per sphere that ANY lane meets (each of the three
+// big spheres is a candidate for ~10 % of lines, so for some lane of almost
+// every wave).  Slot 0 of the first group (the builder puts the largest extra
+// there: the ground, a candidate for almost every line) runs its own sequence
+// first (LEAD).  The candidate rule is order-independent, so the closest hit
+// is the same bits as a scan of the four in any order.
+template <bool OPEN, bool STATS, bool LEAD>
+__device__ __forceinline__ void scan_extras(const RT_CONST pair_geom *__restrict__ g, int slot0,
+                                            const RT_CONST int *__restrict__ orig, const ray_pre &r,
+                                            hit_state &hs, uint32_t &roots) {
+  float h[4], d[4];
+  uint32_t t[4];
+  bool c[4];
 #pragma unroll
-  for (int j = 0; j < NP; ++j) {
+  for (int j = 0; j < 2; ++j) {
     const pair_geom q = cload(g + j);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const float cx = s ? q.cx.y : q.cx.x, cy = s ? q.cy.y : q.cy.x, cz = s ? q.cz.y : q.cz.x;
+      const float ks = s ? q.ks.y : q.ks.x;
       const float hy = fmaf(cy, r.dy.x, r.nk1.x);
       const float gy = fmaf(cy, r.oy2.x, r.o2.x);
       const float hh = fmaf(cz, r.dz.x, fmaf(cx, r.dx.x, hy));
       const float gg = fmaf(cz, r.oz2.x, fmaf(cx, r.ox2.x, gy));
       const float ee = fmaf(hh, hh, -gg);
-      h[2 * j + s] = hh;
-      e[2 * j + s] = ee;
-      ks[2 * j + s] = s ? q.ks.y : q.ks.x;
-      c[2 * j + s] = ee >= ks[2 * j + s];
+      const int k = 2 * j + s;
+      h[k] = hh;
+      d[k] = ee - ks;
+      c[k] = ee >= ks;
+      t[k] = tie2_of<OPEN>((uint32_t)orig[slot0 + k]);
     }
   }
+  constexpr int J0 = LEAD ? 1 : 0;
+  if (LEAD && __builtin_amdgcn_ballot_w64(c[0])) {
+    if (STATS) ++roots;
+    candidate<OPEN>(c[0], h[0], d[0], t[0], hs);
+  }
 #pragma unroll
-  for (int j = 0; j < 2 * NP; ++j) any |= __builtin_amdgcn_ballot_w64(c[j]);
-  if (any) {
-    if (STATS) {
+  for (int round = J0; round < 4; ++round) {
+    // this lane's lowest remaining candidate (the default slot 3 is only
+    // read by lanes with none left, which do not run the sequence)
+    float hh = h[3], dd = d[3];
+    uint32_t tt = t[3];
 #pragma unroll
-      for (int j = 0; j < 2 * NP; ++j) roots += __builtin_amdgcn_ballot_w64(c[j]) != 0 ? 1u : 0u;
+    for (int j = 2; j >= J0; --j)
+      if (c[j]) {
+        hh = h[j];
+        dd = d[j];
+        tt = t[j];
+      }
+    bool taken = false;
+#pragma unroll
+    for (int j = J0; j < 4; ++j) {
+      const bool f = c[j] && !taken;
+      c[j] = c[j] && !f;
+      taken = taken || f;
     }
-#pragma unroll
-    for (int j = 0; j < 2 * NP; ++j) {
-      const int i0 = orig ? orig[slot0 + j] : slot0 + j;
-      candidate<OPEN>(c[j], h[j], e[j] - ks[j], tie2_of<OPEN>((uint32_t)i0), hs);
-    }
+    if (!__builtin_amdgcn_ballot_w64(taken)) break;
+    if (STATS) ++roots;
+    candidate<OPEN>(taken, hh, dd, tt, hs);
   }
 }
 
@@ -670,17 +699,22 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
   const float o2 = dot3(ox, oy, oz, ox, oy, oz);
   const float ox2 = -2.0f * ox, oy2 = -2.0f * oy, oz2 = -2.0f * oz;
   hit_state hs = no_hit();
-  const ray_pre rp{{dx, dx}, {dy, dy}, {dz, dz}, {nk1, nk1},
-                   {o2, o2}, {ox2, ox2}, {oy2, oy2}, {oz2, oz2}};
+  // the per-ray terms, splatted into pairs for the packed scans (the grid
+  // build's extras and walk read the .x halves only)
+  auto splat = [&]() {
+    return ray_pre{{dx, dx}, {dy, dy}, {dz, dz}, {nk1, nk1}, {o2, o2}, {ox2, ox2}, {oy2, oy2}, {oz2, oz2}};
+  };
   // the BVH boxes are padded for ray origins within |O| <= oref (see
   // bvh_builder); a wave-step with any lane beyond that scans everything
   const bool scan_all = !BVH || __builtin_amdgcn_ballot_w64(o2 > p.oref2) != 0;
   if (scan_all) {
     // brute force: 8 spheres (4 pairs) per iteration over the whole array
+    const ray_pre rp = splat();
     for (int k = 0; k < n_pairs; k += 4)
       scan_pairs<OPEN, 4, STATS>(scan_geom + k, 2 * k, nullptr, rp, hs, wc.roots);
     if (STATS) wc.tests += 2 * n_pairs;
   } else {
+    const ray_pre rp = splat();
     // wave-uniform stackless BVH walk: a node is entered if ANY lane's ray
     // meets its (conservatively padded) box before that lane's tmax
     // the reciprocals are clamped to +-1e18 (one v_med3): an exactly
@@ -706,10 +740,14 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
     if (p.layer_mode) {
       // the spheres off the layer (in the final scene the ground and the three
       // big spheres) are scanned first: their hits shorten tmax for the walk
-      for (int k = 0; k < p.n_extra_pairs; k += 2) {
-        if (GRID)
-          scan_pairs_scalar<OPEN, 2, STATS>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, rp, hs, wc.roots);
-        else
+      if (GRID) {
+        // the first group leads with its largest sphere (the builder's order)
+        if (p.n_extra_pairs > 0)
+          scan_extras<OPEN, STATS, true>(geom + p.extra_pair0, 2 * p.extra_pair0, orig, rp, hs, wc.roots);
+        for (int k = 2; k < p.n_extra_pairs; k += 2)
+          scan_extras<OPEN, STATS, false>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, rp, hs, wc.roots);
+      } else {
+        for (int k = 0; k < p.n_extra_pairs; k += 2)
           scan_pairs<OPEN, 2, STATS>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, rp, hs, wc.roots);
       }
       if (STATS) wc.tests += 2 * p.n_extra_pairs;
@@ -724,9 +762,9 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
       const float tyl_f = fmaxf(tyl.x, tyl.y);
       float tyl_fc = fminf(tyl_f, hs.tmax);  // refreshed by walk_step after every leaf
       if (GRID) {  // the layer grid (its own kernel build: no BVH walk code)
-        ray_pre rg = rp;
-        rg.nk1 = fma2(f2{p.layer_cy, p.layer_cy}, rp.dy, rp.nk1);
-        rg.o2 = fma2(f2{p.layer_cy, p.layer_cy}, rp.oy2, rp.o2);
+        ray_pre rg = rp;  // (.x halves only: the walk is per lane)
+        rg.nk1.x = fmaf(p.layer_cy, dy, nk1);
+        rg.o2.x = fmaf(p.layer_cy, oy2, o2);
         if (tyl_n <= tyl_fc) grid_walk<OPEN, STATS, GP>(ox, oz, ix, iz, oix, oiz, tyl_n, tyl_fc, rg, hs, wc);
         return hs;
       }
@@ -961,16 +999,14 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           --segs;
         } else {
         const float px = fmaf(t, dx, ox), py = fmaf(t, dy, oy), pz = fmaf(t, dz, oz);
-        float nx = (px - sr.cx) * sr.inv_r, ny = (py - sr.cy) * sr.inv_r, nz = (pz - sr.cz) * sr.inv_r;
         // set_face_normal (hittable.h:16-19): dot(d, outward) < 0 is, in exact
         // arithmetic, "the entering root was taken" (outward flips for r < 0);
-        // the root form cannot flip sign at grazing incidence in fp32
+        // the root form cannot flip sign at grazing incidence in fp32.  The
+        // flip is folded into the 1/r factor: (p - c) (-1/r) = -((p - c) / r)
+        // exactly, one select instead of three negations
         const bool front = near != (sr.inv_r < 0.0f);
-        if (!front) {
-          nx = -nx;
-          ny = -ny;
-          nz = -nz;
-        }
+        const float fir = front ? sr.inv_r : -sr.inv_r;
+        const float nx = (px - sr.cx) * fir, ny = (py - sr.cy) * fir, nz = (pz - sr.cz) * fir;
         // shared by the material branches (computed once: lanes of one wave
         // usually hit several materials, so the branches all execute)
         const float dn = dot3(dx, dy, dz, nx, ny, nz);
