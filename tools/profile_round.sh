@@ -20,7 +20,7 @@ timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CY
 cd $GRAFT_REPO_ROOT
 # the timed kernel: the LDS-resident layer grid build (bench default); KERNEL overrides
 # (e.g. "render_kernel<false, false, true, false, false, 0>" for --accel layer_bvh)
-K=${KERNEL:-"render_kernel<false, false, true, false, true, 1>"}
+K=${KERNEL:-"render_kernel<false, false, true, false, true, 1, false>"}
 python3 tools/pmc_traffic.py $out/fetch $out/write $out/sq --kernel "$K" --world 1 \
   --workload "$(grep '"metric"' $out/kt.log | tail -1 | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["config"]["workload"])')" \
   --out $out/pmc_traffic.json

@@ -10,7 +10,7 @@ set -e
 tag=$1; shift
 worlds=${*:-"2 4 8"}
 WL="final random-spheres scene 3840x2160 @ 500spp depth 50"
-K=${KERNEL:-"render_kernel<false, false, true, false, true, 1>"}
+K=${KERNEL:-"render_kernel<false, false, true, false, true, 1, false>"}
 for w in $worlds; do
   out=$GRAFT_REPO_ROOT/gpurun_out/share_$tag/w$w
   mkdir -p $out
