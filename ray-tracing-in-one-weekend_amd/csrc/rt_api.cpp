@@ -497,6 +497,8 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
   kp.geom = c->d_bvh_geom;
   kp.nodes = c->d_nodes;
   kp.orig = c->d_orig;
+  kp.extra_geom = c->d_bvh_geom ? c->d_bvh_geom + c->extra_pair0 : nullptr;
+  kp.extra_orig = c->d_orig ? c->d_orig + 2 * (size_t)c->extra_pair0 : nullptr;
   kp.shade = c->d_shade;
   kp.out = accum_rgb;
   kp.counters = c->d_counters;

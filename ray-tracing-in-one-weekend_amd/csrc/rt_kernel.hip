@@ -160,7 +160,9 @@ __device__ f2 g_turn_tab[kTurnTab];
 __device__ __forceinline__ void sincos_turn(float u, float &s, float &c) {
   const float t = u * (float)kTurnTab;
   const float fl = floorf(t);
-  const f2 sc = as_global(g_turn_tab)[(int)fl];
+  // a 32-bit byte offset from the table's base (saddr addressing: no 64-bit
+  // index arithmetic); 0 <= fl < 1024
+  const f2 sc = *(const RT_GLOBAL f2 *)((const RT_GLOBAL char *)as_global(g_turn_tab) + ((uint32_t)fl << 3));
   const float d = (t - fl) * (6.28318530717958648f / (float)kTurnTab);
   const float x2 = d * d;
   const float cd = fmaf(x2, -0.5f, 1.0f);
@@ -443,8 +445,8 @@ __device__ __forceinline__ void scan_extras(const RT_CONST pair_geom *__restrict
     }
   }
   constexpr int J0 = LEAD ? 1 : 0;
-  if (LEAD && __builtin_amdgcn_ballot_w64(c[0])) {
-    if (STATS) ++roots;
+  if (LEAD) {  // (candidate's own lane-mask branch skips a wave with no candidate)
+    if (STATS && __builtin_amdgcn_ballot_w64(c[0])) ++roots;
     candidate<OPEN>(c[0], h[0], d[0], t[0], hs);
   }
 #pragma unroll
@@ -645,7 +647,8 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
     if (GP == kGridLds) {
       lds_f4 *ip = (lds_f4 *)(uintptr_t)((lds_u16 *)(uintptr_t)cell)[0];
       lds_f4 *ie = (lds_f4 *)(uintptr_t)((lds_u16 *)(uintptr_t)cell)[1];
-      asm volatile("" : "+v"(ie));
+      // (both bounds behind one barrier: one wait for the two reads)
+      asm volatile("" : "+v"(ip), "+v"(ie));
       if (ip != ie) do {
         grid_item<OPEN, STATS>(*ip, dx, dz, rl, hs, wc);
         ++ip;
@@ -673,10 +676,14 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
     const float tnext = sx ? tmx : tmz;
     float lim;
     asm("v_min_f32 %0, %1, %2" : "=v"(lim) : "v"(tb), "v"(hs.tmax));
-    if (tnext > lim) break;
+    const bool stop = tnext > lim;
+    // the step is taken before the exit test (a stopping lane's cell and
+    // boundaries are dead after the loop): no exec-mask branch around it
     cell += sx ? dcx : dcz;
-    if (sx) tmx += tdx;
-    else tmz += tdz;
+    tmx = sx ? tmx + tdx : tmx;
+    tmz = sx ? tmz : tmz + tdz;
+    asm volatile("" : "+v"(cell), "+v"(tmx), "+v"(tmz));
+    if (stop) break;
   }
 }
 
@@ -737,15 +744,17 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
       return nodes + (size_t)oct * p.n_nodes;
     };
     const RT_CONST bvh_node *__restrict__ order = GRID ? nullptr : walk_order();
-    if (p.layer_mode) {
+    if (GRID || p.layer_mode) {  // (the grid build runs on layer scenes only)
       // the spheres off the layer (in the final scene the ground and the three
       // big spheres) are scanned first: their hits shorten tmax for the walk
       if (GRID) {
         // the first group leads with its largest sphere (the builder's order)
-        if (p.n_extra_pairs > 0)
-          scan_extras<OPEN, STATS, true>(geom + p.extra_pair0, 2 * p.extra_pair0, orig, rp, hs, wc.roots);
+        // (kparams extra_geom / extra_orig: the host resolved the offsets)
+        const RT_CONST pair_geom *__restrict__ xg = as_const(p.extra_geom);
+        const RT_CONST int *__restrict__ xo = as_const(p.extra_orig);
+        if (p.n_extra_pairs > 0) scan_extras<OPEN, STATS, true>(xg, 0, xo, rp, hs, wc.roots);
         for (int k = 2; k < p.n_extra_pairs; k += 2)
-          scan_extras<OPEN, STATS, false>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, rp, hs, wc.roots);
+          scan_extras<OPEN, STATS, false>(xg + k, 2 * k, xo, rp, hs, wc.roots);
       } else {
         for (int k = 0; k < p.n_extra_pairs; k += 2)
           scan_pairs<OPEN, 2, STATS>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, rp, hs, wc.roots);
@@ -847,20 +856,25 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   // lanes traced its samples in whatever order.
   const uint32_t kend = (s_end > s_begin ? s_end - s_begin : 0u) << 6;
   __shared__ sum_t s_sum[3][kBlock];                    // the tiles' fixed-point pixel sums
-  __shared__ uint32_t s_rowpix[kWavesPerBlock][kTile];  // global pixel index of (x = 0, y)
-  bool own_valid;
+  // per tile row: the global pixel index of (x = 0, y) and how many of the
+  // row's 8 slots are in the frame (0 for a row outside it): one ds_read_b64
+  // per pool take gives both
+  typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+  __shared__ u2v s_rowpix[kWavesPerBlock][kTile];
   {
     const int lane = lane_now();
     const int col = col0 + (lane & (kTile - 1));
     const int lrow = lrow0 + (lane >> 3);
     const int band = lrow / p.row_block;
     const int grow = (band * p.band_stride + p.band_offset) * p.row_block + (lrow - band * p.row_block);
-    own_valid = col < p.width && lrow < p.local_rows && grow < p.height;
-    if ((lane & (kTile - 1)) == 0) s_rowpix[wave][lane >> 3] = (uint32_t)grow * (uint32_t)p.width + (uint32_t)col0;
+    (void)col;
+    if ((lane & (kTile - 1)) == 0) {
+      const bool row_in = lrow < p.local_rows && grow < p.height;
+      const uint32_t ncols = row_in ? (uint32_t)min(kTile, p.width - col0) : 0u;
+      s_rowpix[wave][lane >> 3] = u2v{(uint32_t)grow * (uint32_t)p.width + (uint32_t)col0, ncols};
+    }
   }
   s_sum[0][threadIdx.x] = s_sum[1][threadIdx.x] = s_sum[2][threadIdx.x] = 0u;
-  // slots whose pixel is in the frame (all 64 but in the last tile column / row)
-  const uint64_t vmask = __builtin_amdgcn_ballot_w64(own_valid);
   if (GP == kGridLds) {  // the block's copy of the layer grid (kparams grid_n_items)
     const RT_GLOBAL f4 *gi = as_global(p.grid_items);
     for (int i = (int)threadIdx.x; i < p.grid_n_items; i += kBlock) s_grid_dyn[i] = gi[i];
@@ -891,13 +905,14 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   // wave-uniform values the pool reads once per step, held in VGPRs: as SGPRs
   // they were spilled to VGPR lanes at 8 waves (v_readlane per step)
   uint32_t s_begin_v = s_begin;
-  uint32_t rowpix_v = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t *)&s_rowpix[wave][0];
+  uint32_t rowpix_v = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) u2v *)&s_rowpix[wave][0];
   asm volatile("" : "+v"(s_begin_v), "+v"(rowpix_v));
   auto take = [&](uint32_t k) -> bool {
     slot = k & 63u;
     sample = s_begin_v + (k >> 6);
-    pix = ((const __attribute__((address_space(3))) uint32_t *)(uintptr_t)rowpix_v)[slot >> 3] + (slot & (kTile - 1));
-    return ((vmask >> slot) & 1u) != 0;
+    const u2v e = ((const __attribute__((address_space(3))) u2v *)(uintptr_t)rowpix_v)[slot >> 3];
+    pix = e.x + (slot & (kTile - 1));
+    return (slot & (kTile - 1)) < e.y;
   };
   // (col, global row) of the lane's pixel: col from the tile origin, row by
   // exact division (pix - col) / W
@@ -917,15 +932,17 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
     }
   }
 
-  while (true) {
-    if (!__ballot(alive)) break;
+  // a divergent loop: a lane leaves it when its wave's pool has no item left
+  // for it (the step body then runs under the alive lanes' mask, with no
+  // wave-level any-alive ballot per step)
+  while (alive) {
     hit_state hs = no_hit();
     if (tracing) hs = closest_hit<OPEN, BVH, STATS, GRID, GP>(ox, oy, oz, dx, dy, dz, wc);
     ++steps;
     const int best = best_of<OPEN>(hs);
     // lanes that end their path here (a miss) or hold a slot outside the frame
     // take their next items now: the step's one hash then draws the new camera ray
-    const bool miss = alive && (!tracing || best < 0);
+    const bool miss = !tracing || best < 0;
     uint32_t kn;
     {
       const uint64_t need = __builtin_amdgcn_ballot_w64(miss);
@@ -933,7 +950,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
       knext += (uint32_t)__builtin_popcountll(need);
     }
     bool path_done = false;  // absorbed, or the bounce limit: the lane parks for a step
-    if (alive) {
+    {
       const kparams q = kernargs();  // shading's parameters, re-read per step
       if (tracing) ++segs;
       if (tracing && best < 0) {
@@ -984,7 +1001,10 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         const float ox2 = -2.0f * ox, oy2 = -2.0f * oy, oz2 = -2.0f * oz;
         const float tmax = hs.tmax;
         const bool near = near_of(hs) != 0;
-        const shade_rec sr = cload_g(as_global(q.shade) + best);
+        // a 32-bit byte offset from the records' base (saddr addressing)
+        static_assert(sizeof(shade_rec) == 64, "best << 6");
+        const shade_rec sr = cload_g((const RT_GLOBAL shade_rec *)((const RT_GLOBAL char *)as_global(q.shade) +
+                                                                   ((uint32_t)best << 6)));
         float b;
         const float t = refine_root(sr, tmax, near, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2, b);
         // A refined root before t_min on a sphere the ray moves away from
@@ -1012,9 +1032,13 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         const float dn = dot3(dx, dy, dz, nx, ny, nz);
         float rx, ry, rz;
         reflect3(dx, dy, dz, nx, ny, nz, dn, rx, ry, rz);
-        float sx, sy, sz;
+        // three independent material blocks, each under its own lane mask (an
+        // if / else-if chain compiles to a structurised exec-mask cascade of
+        // ~35 scalar instructions; kinds are 0..2, rt_scene_upload checks)
+        float sx = rx, sy = ry, sz = rz;
         bool scattered = true;
-        if (sr.kind == RT_LAMBERTIAN) {
+        const uint32_t kind = sr.kind;
+        if (kind == RT_LAMBERTIAN) {
           // The opaque-inside rule: a sealed lambertian
           // sphere (no other ball overlaps its ball, rt_accel.cpp
           // sealed_spheres) hit at its exiting root -- the ray started inside
@@ -1037,7 +1061,8 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
             sy = ny;
             sz = nz;
           }
-        } else if (sr.kind == RT_METAL) {
+        }
+        if (kind == RT_METAL) {
           // material.h:40-46
           float fz = sr.param;
           if (!METAL_UNIT) fz *= ball_radius(r);  // random_in_unit_sphere
@@ -1045,19 +1070,15 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           sy = fmaf(fz, uy, ry);
           sz = fmaf(fz, uz, rz);
           scattered = dot3(sx, sy, sz, nx, ny, nz) > 0.0f;
-        } else {
+        }
+        if (kind >= RT_DIELECTRIC) {
           // dielectric, material.h:57-87 (r0 is the same for ior and 1/ior)
           const float ratio = front ? sr.inv_param : sr.param;
           const float cos_t = fminf(-dn, 1.0f);
           // ratio sin > 1 (material.h:64), squared: no square root
           const bool cannot = (ratio * ratio) * fmaf(-cos_t, cos_t, 1.0f) > 1.0f;
-          if (cannot || schlick(cos_t, sr.r0) > unif(r.x)) {
-            sx = rx;
-            sy = ry;
-            sz = rz;
-          } else {
-            refract3(dx, dy, dz, nx, ny, nz, cos_t, ratio, sx, sy, sz);
-          }
+          // (s = the reflection, set above, unless it refracts)
+          if (!(cannot || schlick(cos_t, sr.r0) > unif(r.x))) refract3(dx, dy, dz, nx, ny, nz, cos_t, ratio, sx, sy, sz);
         }
         // attenuation = albedo (dielectrics store 1,1,1: the product is exact)
         thr *= sr.ar;
@@ -1095,7 +1116,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
     if (path_done) tracing = false;
     // one normalize3 per lane and step: the bounce direction or the new
     // camera ray's (a finished lane's is unused)
-    if (alive) normalize3(dx, dy, dz);
+    normalize3(dx, dy, dz);
   }
 
   const int lane = lane_now();
@@ -1120,10 +1141,13 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   }
   // one atomic per wave for the counters
   uint32_t s = segs;
+  // wave-steps: the most any lane of the wave looped
+  uint32_t ws = steps;
   uint64_t lt = wc.tests, lb = wc.boxes, lh = wc.box_hits, lr = wc.roots;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     s += __shfl_xor(s, off);
+    ws = max(ws, (uint32_t)__shfl_xor(ws, off));
     if (STATS) {
       lt += __shfl_xor(lt, off);
       lb += __shfl_xor(lb, off);
@@ -1143,7 +1167,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
     }
     unsigned long long *counters = kernargs().counters + 8 * (blockIdx.x & (kCounterSlots - 1));
     atomicAdd(&counters[0], (unsigned long long)s);
-    atomicAdd(&counters[1], (unsigned long long)steps);
+    atomicAdd(&counters[1], (unsigned long long)ws);
     if (STATS) {
       atomicAdd(&counters[2], (unsigned long long)lt);
       atomicAdd(&counters[3], (unsigned long long)lb);

@@ -165,6 +165,11 @@ struct kparams {
   // u16 item-start LDS addresses (cell i's items are [start_i, start_{i+1}));
   // kGridCells copies n_cells + 1 u16 item-start INDICES only
   int grid_n_items, grid_n_cells;
+  // layer mode: the extras' first scan pair and its slots' original indices
+  // (geom + extra_pair0, orig + 2 extra_pair0), resolved on the host so the
+  // kernel does no 64-bit index arithmetic per step
+  const struct pair_geom *extra_geom;
+  const int *extra_orig;
 };
 
 // LDS bytes of the grid copy of one block
@@ -176,7 +181,7 @@ __host__ __device__ constexpr size_t grid_lds_bytes(int placement, long long n_i
 // LDS budget of the grid copy: with render_kernel's static LDS (the tiles'
 // pixel sums and row indices) a 256-thread block stays within 20 KB, so 8
 // blocks (8 waves per SIMD) still fit in the CU's 160 KB
-constexpr size_t kStaticLds = 3 * kBlock * 4 + kWavesPerBlock * kTile * 4;
+constexpr size_t kStaticLds = 3 * kBlock * 4 + kWavesPerBlock * kTile * 8;  // sums + row table (pixel base, valid columns)
 constexpr size_t kGridLdsMax = 160 * 1024 / 8 - kStaticLds;
 // WIDE builds hold 64-bit pixel sums: 3 KB more static LDS
 constexpr size_t kGridLdsMaxWide = kGridLdsMax - 3 * kBlock * 4;
