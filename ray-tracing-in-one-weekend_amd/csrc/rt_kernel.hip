@@ -664,10 +664,14 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
         k = ce >> 4;
         ke = k + (ce & 15u);
       }
-      if (k != ke) do {
-        grid_item<OPEN, STATS>(items[k], dx, dz, rl, hs, wc);
-        ++k;
-      } while (k != ke);
+      // byte offsets from the items' base (saddr loads: no 64-bit address
+      // per item; the loop steps the offset by 16)
+      uint32_t ko = k << 4;
+      const uint32_t koe = ke << 4;
+      if (ko != koe) do {
+        grid_item<OPEN, STATS>(*(const RT_GLOBAL f4 *)((const RT_GLOBAL char *)items + ko), dx, dz, rl, hs, wc);
+        ko += 16;
+      } while (ko != koe);
     }
     // one compare picks the step axis and the next boundary (tmx == tmz
     // steps z, as before); v_min_f32 written out: fminf would first
