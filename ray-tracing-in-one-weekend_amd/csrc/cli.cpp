@@ -237,6 +237,8 @@ int main(int argc, char **argv) {
   for (int g = 0; g < o.gpus; ++g) {
     check(rt_context_create(jobs[g].device, &ctxs[g]), "rt_context_create");
     check(rt_scene_upload(ctxs[g], &view), "rt_scene_upload");
+    // the layer grid's cell size for this device's share (scheduling only)
+    check(rt_tune_grid(ctxs[g], &cam, &jobs[g].params, nullptr), "rt_tune_grid");
   }
   const bool use_rccl = o.gather == "rccl" || (o.gather == "auto" && o.gpus > 1);
   // Every device renders its tile (fp32 sums) and tonemaps it on the device
