@@ -856,7 +856,11 @@ int rt_tune_grid(rt_context *c, const rt_camera *cam, const rt_params *prm, doub
   RT_HIP(hipDeviceSynchronize());
   RT_HIP(ensure_frame(c, 3 * (size_t)prm->width * (size_t)prm->local_rows));
   // the render's own variant (placement, sum format), one unit, float stores,
-  // launch order, about 2^26 samples (at most 16 per pixel, at most spp)
+  // launch order.  Each block gets about the samples per pixel of a render
+  // (min(spp, 128)), over every S-th block (a uniform subset of the tiles) so
+  // that a candidate's pilot stays near 2^27 samples: with a few samples per
+  // pixel over all tiles, each block's copy of the grid into LDS would weigh
+  // far more than in the render and favour the coarsest grid.
   rtk::kparams kp;
   fill_kparams(c, cam, prm, c->d_frame, kp);
   const sum_fmt fmt = sum_format(prm->spp, prm->max_depth, c->max_albedo);
@@ -868,11 +872,15 @@ int rt_tune_grid(rt_context *c, const rt_camera *cam, const rt_params *prm, doub
   kp.units = 1;
   kp.sum_atomic = 0;
   kp.s_lo = 0;
-  kp.s_cnt = (int)std::max<long long>(
-      1, std::min<long long>({std::llround((double)(1 << 26) / (double)px), 16LL, (long long)prm->spp}));
+  kp.s_cnt = std::min(prm->spp, 128);
   const int tiles_y = (prm->local_rows + rtk::kTile - 1) / rtk::kTile;
   const long long tiles = (long long)kp.tiles_x * tiles_y;
-  const unsigned blocks = (unsigned)((tiles + rtk::kWavesPerBlock - 1) / rtk::kWavesPerBlock);
+  const long long all_blocks = (tiles + rtk::kWavesPerBlock - 1) / rtk::kWavesPerBlock;
+  const long long stride =
+      std::max<long long>(1, std::llround((double)px * kp.s_cnt / (double)(1 << 27)));
+  kp.block_stride = (int)std::min<long long>(stride, all_blocks);
+  kp.block_base = kp.block_stride / 2;
+  const unsigned blocks = (unsigned)((all_blocks - kp.block_base + kp.block_stride - 1) / kp.block_stride);
   const size_t n = c->grid_alts.size();
   constexpr int kPasses = 2;
   // scratch counters and timing events, released on every path

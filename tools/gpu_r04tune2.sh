@@ -1,0 +1,16 @@
+#!/bin/bash
+# rt_tune_grid (render-like samples per block in its pilots): its GPU test,
+# the C4 rank-0 share and the headline frame with and without it, same box
+set -e
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_configs_gpu.py -k "grid_tune" > gpurun_out/r04tune2_test.log 2>&1
+for k in 1 2; do
+  timeout -k 10 120 python tools/rank_share.py --preset c4 --world 8 --rank 0 --spp 200 --reps 2 --no-grid-tune >> gpurun_out/r04tune2_c4_200.log 2>&1
+  timeout -k 10 120 python tools/rank_share.py --preset c4 --world 8 --rank 0 --spp 200 --reps 2 >> gpurun_out/r04tune2_c4_200.log 2>&1
+done
+for k in 1 2; do
+  timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 --warmup 2 --no-grid-tune >> gpurun_out/r04tune2_bench.log 2>&1
+  timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 --warmup 2 >> gpurun_out/r04tune2_bench.log 2>&1
+done
+timeout -k 10 180 python tools/rank_share.py --preset c4 --world 8 --rank 0 7 --flags PILOT_SCHEDULE > gpurun_out/r04tune2_share_c4.log 2>&1
+echo done
