@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--pilot", action="store_true",
                     help="RT_FLAG_PILOT_SCHEDULE; every share is rendered twice and the second "
                          "(with the cached tile order) is timed")
+    ap.add_argument("--no-grid-tune", action="store_true",
+                    help="keep the builder's grid (bench.py tunes it per rank: rt_tune_grid)")
     a = ap.parse_args()
     import rtow
     ctx = rtow.Context(0)
@@ -32,8 +34,11 @@ def main():
     cam = rtow.camera_cpu(aspect=a.w / a.h)
     flags = rtow.RT_FLAG_ACCEL_BVH | (rtow.RT_FLAG_PILOT_SCHEDULE if a.pilot else 0)
     reps = 2 if a.pilot else 1
+    p = rtow.make_params(a.w, a.h, a.spp, seed=0, flags=flags)
+    if not a.no_grid_tune:
+        ctx.tune_grid(cam, p)
     for _ in range(reps):
-        _, st = ctx.render(cam, rtow.make_params(a.w, a.h, a.spp, seed=0, flags=flags))
+        _, st = ctx.render(cam, p)
     full = st.kernel_ms
     print(json.dumps({"world": 1, "kernel_ms": round(full, 2)}), flush=True)
     for g in a.world:
@@ -42,6 +47,8 @@ def main():
             for r in range(g):
                 p = rtow.make_params(a.w, a.h, a.spp, seed=0, flags=flags, rank=r, world=g,
                                      row_block=a.row_block, units=u)
+                if not a.no_grid_tune:
+                    ctx.tune_grid(cam, p)
                 for _ in range(reps):
                     _, st = ctx.render(cam, p)
                 ms.append(st.kernel_ms)
