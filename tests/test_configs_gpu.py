@@ -317,13 +317,13 @@ def test_grid_tune_candidates_render_the_oracle_image(rtow, gpu_ctx, oracle, hal
     s0 = rtow.accel_info(scene)["grid_scale_milli"] / 1000.0
     try:
         for k in (0, 3, 7, 15, 30):
-            gpu_ctx.upload(scene, grid_scale=s0 * (1.0 + 0.01 * k))
+            gpu_ctx.upload(scene, grid_mode="auto", grid_scale=s0 * (1.0 + 0.01 * k))
             got, st = gpu_ctx.render(cam, p)
             assert np.array_equal(got, want), (k, int((got != want).sum()))
             assert st.segments == segs, k
     finally:
         gpu_ctx.set_option(rtow.RT_OPT_GRID_SCALE, 0)
-    gpu_ctx.upload(scene)
+    gpu_ctx.upload(scene, grid_mode="auto")
     cands = gpu_ctx.grid_candidates()
     assert len(cands) >= 2 and all(np.isnan(m) for _, m in cands)
     assert gpu_ctx.tune_grid(cam, band_params(rtow, W, H, 64, 4, 1, rows=8, seed=515)) == cands[0][0]
