@@ -283,6 +283,7 @@ def main():
         grid_tune = {"cell_scale": round(g, 4), "candidates": len(cands),
                      "pilot_ms_builder_grid": round(base_ms, 4) if base_ms is not None else None,
                      "pilot_ms_kept_grid": round(kept_ms, 4) if kept_ms is not None else None,
+                     "pilot_ms": {f"{s_:.4f}": round(m, 4) for s_, m in cands},
                      "wall_ms": round((time.perf_counter() - t_tune) * 1e3, 1)}
     tile = torch.zeros((params.local_rows, W, 3), dtype=torch.float32, device=dev)
     # the step ends like the drop-in CLI's: write_color on the device (src/cpu

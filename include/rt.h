@@ -294,7 +294,7 @@ int rt_render(rt_context *ctx, const rt_camera *cam, const rt_params *params,
  * spheres the frame's rays meet most moves the walk's cost by several per
  * cent, so this renders a short pilot of (cam, params) --
  * min(spp, 128) samples per pixel on a uniform subset of the tiles, about
- * 2^27 samples, into a context-owned buffer -- twice with every candidate,
+ * 2^27 samples, into a context-owned buffer -- three times with every candidate,
  * keeps the fastest for
  * the context's following renders and stores its scale in *grid_scale (may
  * be NULL; 0 without a grid).  Synchronous; waits for the device first.

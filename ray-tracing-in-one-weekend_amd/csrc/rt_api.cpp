@@ -882,7 +882,7 @@ int rt_tune_grid(rt_context *c, const rt_camera *cam, const rt_params *prm, doub
   kp.block_base = kp.block_stride / 2;
   const unsigned blocks = (unsigned)((all_blocks - kp.block_base + kp.block_stride - 1) / kp.block_stride);
   const size_t n = c->grid_alts.size();
-  constexpr int kPasses = 2;
+  constexpr int kPasses = 3;
   // scratch counters and timing events, released on every path
   struct scratch {
     unsigned long long *ctr = nullptr;
