@@ -84,8 +84,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pilot", action="store_true",
                     help="launch tiles in index order (no RT_FLAG_PILOT_SCHEDULE)")
-    ap.add_argument("--no-grid-tune", action="store_true",
-                    help="keep the builder's layer-grid cell size (no rt_tune_grid)")
+    ap.add_argument("--grid-tune", action="store_true",
+                    help="pick the layer grid's cell size by rt_tune_grid's pilots before the warmup "
+                         "(opt-in: its picks do not reliably carry over to the full frame, DESIGN 3.3)")
     ap.add_argument("--out", default="", help="write the gathered frame as PPM (P6 if .pgm/.p6)")
     a = ap.parse_args()
     if a.preset:
@@ -270,11 +271,11 @@ def main():
         params.flags |= rtow.RT_FLAG_ACCEL_BVH
     if a.accel == "layer_bvh":
         params.flags |= rtow.RT_FLAG_LAYER_BVH
-    # the layer grid's cell size for this frame geometry (rt_tune_grid: a short
-    # pilot per candidate, before the warmup; the image is the same for every
-    # candidate)
+    # --grid-tune: the layer grid's cell size for this frame geometry
+    # (rt_tune_grid: pilots per candidate, before the warmup; the image is the
+    # same for every candidate)
     grid_tune = None
-    if a.accel == "bvh" and not a.no_grid_tune:
+    if a.accel == "bvh" and a.grid_tune:
         t_tune = time.perf_counter()
         g = ctx.tune_grid(cam, params)
         cands = ctx.grid_candidates()

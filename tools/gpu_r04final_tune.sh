@@ -1,3 +1,5 @@
+# (run while bench.py, rank_share.py and rank_times.py tuned the grid by default; they now need
+#  --grid-tune for that, and --no-grid-tune is gone: the untuned runs are the default)
 # round 4, final kernel with rt_tune_grid: GPU tests, smoke, bench, rocprofv3 kernel trace + PMC
 # passes of the headline frame and the 1/2, 1/4, 1/8 shares, C1, every rank's
 # share at N = 2, 4, 8, C3 / C4 rank shares at their own spp

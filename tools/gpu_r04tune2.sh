@@ -1,4 +1,6 @@
 #!/bin/bash
+# (run while bench.py, rank_share.py and rank_times.py tuned the grid by default; they now need
+#  --grid-tune for that, and --no-grid-tune is gone: the untuned runs are the default)
 # rt_tune_grid (render-like samples per block in its pilots): its GPU test,
 # the C4 rank-0 share and the headline frame with and without it, same box
 set -e

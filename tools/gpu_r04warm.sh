@@ -1,4 +1,6 @@
 #!/bin/bash
+# (run while bench.py, rank_share.py and rank_times.py tuned the grid by default; they now need
+#  --grid-tune for that, and --no-grid-tune is gone: the untuned runs are the default)
 # Is the tuned bench's gain the grid or the extra GPU work before the warmup?
 set -e
 mkdir -p gpurun_out

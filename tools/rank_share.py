@@ -36,7 +36,7 @@ def main():
     ap.add_argument("--flags", default="", help="extra '+'-joined RT_FLAG_ names")
     ap.add_argument("--units", type=int, default=0, help="rt_params.units (0: automatic)")
     ap.add_argument("--grid-scale", type=float, default=0.0)
-    ap.add_argument("--no-grid-tune", action="store_true", help="keep the builder's grid (no rt_tune_grid)")
+    ap.add_argument("--grid-tune", action="store_true", help="rt_tune_grid before the renders (opt-in)")
     ap.add_argument("--row-block", type=int, default=8, help="rows per interleaved band")
     a = ap.parse_args()
     import rtow
@@ -54,7 +54,7 @@ def main():
     for r in a.rank:
         p = rtow.make_params(w, h, spp, seed=0, flags=flags, rank=r, world=a.world, units=a.units,
                              row_block=a.row_block)
-        g = 0.0 if a.no_grid_tune else ctx.tune_grid(cam, p)
+        g = ctx.tune_grid(cam, p) if a.grid_tune else 0.0
         for _ in range(a.reps):
             t = time.perf_counter()
             img, st = ctx.render(cam, p)
