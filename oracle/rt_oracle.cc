@@ -338,8 +338,9 @@ inline float dot3(float ax, float ay, float az, float bx, float by, float bz) {
   return fmaf_(az, bz, fmaf_(ay, by, ax * bx));
 }
 
-// the kernel's normalize3: integer-seeded inverse sqrt + 3 Newton steps
-void normalize3(float &x, float &y, float &z) {
+// the kernel's normalize3: integer-seeded inverse sqrt + 3 Newton steps;
+// returns the length it divided by, l2 * r (|x| within a few ulp)
+float normalize3(float &x, float &y, float &z) {
   const float l2 = dot3(x, y, z, x, y, z);
   uint32_t i;
   std::memcpy(&i, &l2, 4);
@@ -351,7 +352,16 @@ void normalize3(float &x, float &y, float &z) {
   x *= r;
   y *= r;
   z *= r;
+  return l2 * r;
 }
+
+// t_min of a ray whose direction was normalised from length len (DESIGN.md
+// 2, step 2): the reference tests its roots against 0.001 in units of the
+// ray's UNnormalised direction (src/cpu/main.cc:19 world.hit(r, 0.001, ..);
+// src/gpu/camera.h:117 interval(0.001, inf); sphere.h:37-41 roots in units of
+// d), i.e. 0.001 |d| in world units on the normalised ray.  tmin_world: the
+// round-1..4 specification, 0.001 world units whatever |d| was.
+inline float tmin_of(bool tmin_world, float len) { return tmin_world ? 0.001f : 0.001f * len; }
 
 struct kscene {
   std::vector<float> cx, cy, cz, ks, inv_r, radius, ar, ag, ab, param, inv_param, r0;
@@ -369,6 +379,7 @@ struct kctx {
   double *exact = nullptr;  // rto_kernel_render_exact: fp64 sums of the unquantised radiance
   const float *out0 = nullptr;  // ... indexed like the frame tile out0
   bool no_dither = false;   // ... and the format without stochastic rounding (truncation only)
+  bool tmin_world = false;  // t_min in world units (the round-4 specification, RTO_OPT_TMIN_WORLD)
 };
 
 // the sum format's dither draw (rt_kernel.hip dither_u): pcg4d keyed by the
@@ -377,8 +388,9 @@ inline float dither_u(uint32_t pix, uint32_t sample, uint32_t seed32) {
   return unif(pcg4d(pix, sample, 0u, ~seed32).x);
 }
 
-void camera_ray(const kctx &k, uint32_t pix, int col, int grow, uint32_t sample, float o[3],
-                float d[3]) {
+// returns the ray's t_min (tmin_of its unnormalised direction's length)
+float camera_ray(const kctx &k, uint32_t pix, int col, int grow, uint32_t sample, float o[3],
+                 float d[3]) {
   const rt_camera &c = *k.cam;
   u4 r = pcg4d(pix, sample, 0u, k.seed32);
   float u1 = unif(r.x), u2 = unif(r.y);
@@ -403,7 +415,7 @@ void camera_ray(const kctx &k, uint32_t pix, int col, int grow, uint32_t sample,
     for (int a = 0; a < 3; ++a) o[a] = fmaf_(ddy, c.lens_v[a], fmaf_(ddx, c.lens_u[a], o[a]));
   }
   for (int a = 0; a < 3; ++a) d[a] = t[a] - o[a];
-  normalize3(d[0], d[1], d[2]);
+  return tmin_of(k.tmin_world, normalize3(d[0], d[1], d[2]));
 }
 
 // one pixel, all samples; returns number of closest-hit queries
@@ -442,7 +454,7 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
   uint64_t q[3] = {0u, 0u, 0u};
   for (uint32_t sample = 0; sample < (uint32_t)k.p->spp; ++sample) {
     float o[3], d[3];
-    camera_ray(k, pix, col, grow, sample, o, d);
+    float tmin = camera_ray(k, pix, col, grow, sample, o, d);
     float th[3] = {1.0f, 1.0f, 1.0f};
     for (int depth = 0;;) {
       ++segs;
@@ -486,9 +498,9 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
             // does, stated so that any visiting order gives the same winner)
             const float sq = sqrt_k(eb[j]);
             const float t0 = h - sq, t1 = h + sq;
-            const bool use0 = k.open ? t0 > 0.001f : t0 >= 0.001f;
+            const bool use0 = k.open ? t0 > tmin : t0 >= tmin;
             const float root = use0 ? t0 : t1;
-            const bool above = k.open ? root > 0.001f : root >= 0.001f;
+            const bool above = k.open ? root > tmin : root >= tmin;
             const bool closer = root < tmax || (root == tmax && (k.open ? (long)i < best : (long)i > best));
             if (tr)
               std::fprintf(g_trace, "   cand %zu disc=%.9g t0=%.9g t1=%.9g root=%.9g above=%d closer=%d\n", i,
@@ -545,7 +557,8 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
         // spheres far from the origin it can trap the path inside the
         // sphere).  Not a segment: the ray moves on to the scan's root point
         // (>= t_min further, so this ends) and walks again, same direction.
-        if (t < 0.001f && bb > 0.0f) {
+        // (the ray keeps its t_min: same direction, same parameter unit)
+        if (t < tmin && bb > 0.0f) {
           if (tr) std::fprintf(g_trace, "  spurious best %ld t %.9g: skipped\n", best, tmax);
           for (int a = 0; a < 3; ++a) o[a] = fmaf_(tmax, d[a], o[a]);
           normalize3(d[0], d[1], d[2]);
@@ -634,7 +647,7 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
         o[a] = p[a];
         d[a] = sd[a];
       }
-      normalize3(d[0], d[1], d[2]);
+      tmin = tmin_of(k.tmin_world, normalize3(d[0], d[1], d[2]));
     }
   }
   for (int a = 0; a < 3; ++a) acc[a] = (wide ? (float)q[a] : (float)(uint32_t)q[a]) * qinv;
@@ -753,7 +766,10 @@ unsigned long long gpuref_pixel(const kctx &k, int col, int grow, float acc[3], 
       o.z = fmaf_(dy, c.lens_v[2], fmaf_(dx, c.lens_u[2], o.z));
     }
     gvec d = gsub(tgt, o);
-    if (!unnorm) normalize3(d.x, d.y, d.z);
+    // t_min in units of the unnormalised direction (tmin_of); with GREF_UNNORM
+    // the roots are in those units already
+    float tmin = 0.001f;
+    if (!unnorm) tmin = tmin_of(k.tmin_world, normalize3(d.x, d.y, d.z));
     gvec att{1.0f, 1.0f, 1.0f};
     gvec col3{0.0f, 0.0f, 0.0f};
     for (int depth = 0; depth < k.p->max_depth; ++depth) {
@@ -774,9 +790,9 @@ unsigned long long gpuref_pixel(const kctx &k, int col, int grow, float acc[3], 
           if (disc < 0.0f) continue;
           const float sq = std::sqrt(disc);
           float root = (-hb - sq) / a;
-          if (!(root > 0.001f && root < tbest)) {  // interval::surrounds
+          if (!(root > tmin && root < tbest)) {  // interval::surrounds
             root = (-hb + sq) / a;
-            if (!(root > 0.001f && root < tbest)) continue;
+            if (!(root > tmin && root < tbest)) continue;
           }
           tbest = root;
           best = (long)i;
@@ -801,9 +817,9 @@ unsigned long long gpuref_pixel(const kctx &k, int col, int grow, float acc[3], 
           if (!(e >= sc.ks[i])) continue;
           const float sq = sqrt_k(e - sc.ks[i]);
           const float t0 = h - sq, t1 = h + sq;
-          const bool use0 = t0 > 0.001f;
+          const bool use0 = t0 > tmin;
           const float root = use0 ? t0 : t1;
-          if (root > 0.001f && (root < tbest || (root == tbest && (long)i < best))) {
+          if (root > tmin && (root < tbest || (root == tbest && (long)i < best))) {
             tbest = root;
             near = use0;
             best = (long)i;
@@ -833,7 +849,7 @@ unsigned long long gpuref_pixel(const kctx &k, int col, int grow, float acc[3], 
             const float tr = near ? std::fmin(ta, tb) : std::fmax(ta, tb);
             if (std::isfinite(tr)) t = tr;
           }
-          if (t < 0.001f && bb > 0.0f) {  // spurious root: move on, not a segment
+          if (t < tmin && bb > 0.0f) {  // spurious root: move on, not a segment
             o = gfma(tbest, d, o);
             --segs;
             --depth;
@@ -896,7 +912,7 @@ unsigned long long gpuref_pixel(const kctx &k, int col, int grow, float acc[3], 
       att = gvec{att.x * sc.ar[b], att.y * sc.ag[b], att.z * sc.ab[b]};
       o = p;
       d = sd;
-      if (!unnorm) normalize3(d.x, d.y, d.z);
+      if (!unnorm) tmin = tmin_of(k.tmin_world, normalize3(d.x, d.y, d.z));
     }
     const float v[3] = {col3.x, col3.y, col3.z};
     for (int j = 0; j < 3; ++j) {
@@ -1095,7 +1111,7 @@ int reference_render_world(dworld &w, rng64 &r, d3 lookfrom, d3 lookat, double a
 }  // namespace
 
 int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
-                            float *out, double *exact, int no_dither, unsigned long long *segments,
+                            float *out, double *exact, int opts, unsigned long long *segments,
                             int threads) {
   if (!scene || !cam || !p || !out || p->width < 1 || p->height < 1 || p->row_block < 1 ||
       p->band_stride < 1 || p->local_rows < 0 || p->spp < 0 || p->spp >= (1 << 24))
@@ -1105,7 +1121,8 @@ int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, co
          (p->flags & RT_FLAG_OPEN_INTERVAL) != 0, (p->flags & RT_FLAG_METAL_UNIT_VECTOR) != 0};
   k.exact = exact;
   k.out0 = out;
-  k.no_dither = no_dither != 0;
+  k.no_dither = (opts & RTO_OPT_NO_DITHER) != 0;
+  k.tmin_world = (opts & RTO_OPT_TMIN_WORLD) != 0;
   if (exact) std::memset(exact, 0, 3 * sizeof(double) * (size_t)p->local_rows * (size_t)p->width);
   if (threads < 1) {
     // the machine's cores, but no more than OMP_NUM_THREADS (16 on the GPU

@@ -27,11 +27,17 @@ int rto_kernel_render(const rt_scene_view *scene, const rt_camera *cam, const rt
                       float *out, unsigned long long *segments, int threads);
 /* The same, plus (exact != NULL) each pixel's fp64 sum of the unquantised
  * sample radiances (3 doubles per pixel, laid out like out) -- the reference's
- * own accumulation (src/cpu/main.cc:114-119) of the same samples -- and, with
- * no_dither, the sum format without its stochastic rounding (truncation at
- * every spp: the round-2 format, for the test that shows why it changed). */
+ * own accumulation (src/cpu/main.cc:114-119) of the same samples.  opts bits
+ * select superseded forms of the specification, for the tests and attribution
+ * tools that show why they changed:
+ *   RTO_OPT_NO_DITHER  the sum format without its stochastic rounding
+ *                      (truncation at every spp: the round-2 format);
+ *   RTO_OPT_TMIN_WORLD t_min = 0.001 in world units on the normalised ray (the
+ *                      round-1..4 form) instead of 0.001 in units of the
+ *                      unnormalised direction, as the reference tests it. */
+enum { RTO_OPT_NO_DITHER = 1, RTO_OPT_TMIN_WORLD = 2 };
 int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
-                            float *out, double *exact, int no_dither, unsigned long long *segments,
+                            float *out, double *exact, int opts, unsigned long long *segments,
                             int threads);
 /* fp64 final scene rows: kind, cx, cy, cz, r, albedo rgb, param (9 doubles). */
 /* src/gpu's own per-sample arithmetic with switches (mode: GREF_* bits in

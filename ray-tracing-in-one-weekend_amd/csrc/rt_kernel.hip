@@ -201,7 +201,11 @@ __device__ __forceinline__ void polar(float a, float u, float &x, float &y) {
 // restatement reproduces it bit for bit, and ~12 VALU instead of a correctly
 // rounded sqrt followed by a correctly rounded division (~28).  |result| is 1
 // within a few ulp; l2 is never 0 or inf here ("Kernel").
-__device__ __forceinline__ void normalize3(float &x, float &y, float &z) {
+// Returns the ray's t_min: 0.001 in units of the unnormalised direction, as
+// the reference tests its roots (src/cpu/main.cc:19 world.hit(r, 0.001, ..),
+// sphere.h:37-41; src/gpu/camera.h:117 interval(0.001, inf)), i.e. 0.001 |x|
+// on the normalised ray, with |x| = l2 r.
+__device__ __forceinline__ float normalize3(float &x, float &y, float &z) {
   const float l2 = fmaf(z, z, fmaf(y, y, x * x));
   float r = __uint_as_float(0x5f375a86u - (__float_as_uint(l2) >> 1));
   const float h = 0.5f * l2;
@@ -210,6 +214,7 @@ __device__ __forceinline__ void normalize3(float &x, float &y, float &z) {
   x *= r;
   y *= r;
   z *= r;
+  return 0.001f * (l2 * r);
 }
 
 __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {
@@ -282,20 +287,14 @@ __device__ __forceinline__ void camera_dir(const kparams &p, const uint4 r, floa
   dz = tz - oz;
 }
 
-// the whole camera ray for r = pcg4d(pix, sample, 0, seed32)
-__device__ __forceinline__ void camera_ray(const kparams &p, const uint4 r, int col, int grow,
-                                           float &ox, float &oy, float &oz,
-                                           float &dx, float &dy, float &dz) {
+// the whole camera ray for r = pcg4d(pix, sample, 0, seed32); returns its t_min
+__device__ __forceinline__ float camera_ray(const kparams &p, const uint4 r, int col, int grow,
+                                            float &ox, float &oy, float &oz,
+                                            float &dx, float &dy, float &dz) {
   float ddx = 0.0f, ddy = 0.0f;
   if (p.cam.has_lens) polar(unif(r.z), unif(r.w), ddx, ddy);
   camera_dir(p, r, ddx, ddy, col, grow, ox, oy, oz, dx, dy, dz);
-  normalize3(dx, dy, dz);
-}
-
-template <bool OPEN>
-__device__ __forceinline__ bool in_range(float t, float tmin, float tmax) {
-  if (OPEN) return (t > tmin) & (t < tmax);   // interval::surrounds
-  return (t >= tmin) & (t <= tmax);           // src/cpu/sphere.h:38-42
+  return normalize3(dx, dy, dz);
 }
 
 // This lane's index in its wave, recomputed where it is needed (volatile: not
@@ -335,16 +334,16 @@ __device__ __forceinline__ hit_state no_hit() { return hit_state{__builtin_huge_
 // the FIRST for src/gpu's open one.  This makes the result independent of the
 // order spheres are visited in: brute-force scan and BVH traversal agree bit
 // for bit.
-// tie2 = tie2_of<OPEN>(index).
+// tie2 = tie2_of<OPEN>(index); tmin = the ray's t_min (normalize3).
 template <bool OPEN>
-__device__ __forceinline__ void candidate(bool c, float h, float disc, uint32_t tie2, hit_state &hs) {
+__device__ __forceinline__ void candidate(bool c, float h, float disc, uint32_t tie2, float tmin, hit_state &hs) {
   if (c) {
     const float sq = sqrt_k(disc);
     const float t0 = h - sq, t1 = h + sq;
-    const bool use0 = OPEN ? (t0 > 0.001f) : (t0 >= 0.001f);
+    const bool use0 = OPEN ? (t0 > tmin) : (t0 >= tmin);
     const float root = use0 ? t0 : t1;
     // root >= t_min  <=>  t1 >= t_min (t1 >= t0; with use0, t0 >= t_min)
-    const bool above = OPEN ? (t1 > 0.001f) : (t1 >= 0.001f);
+    const bool above = OPEN ? (t1 > tmin) : (t1 >= tmin);
     const uint32_t lo = tie2 + (use0 ? 1u : 0u);
     const uint64_t key = ((uint64_t)__float_as_uint(root) << 32) | lo;
     const uint64_t cur = ((uint64_t)__float_as_uint(hs.tmax) << 32) | hs.lo;
@@ -371,7 +370,7 @@ struct ray_pre {
 template <bool OPEN, int NP, bool STATS, bool NOY = false>
 __device__ __forceinline__ void scan_pairs(const RT_CONST pair_geom *__restrict__ g, int slot0,
                                            const RT_CONST int *__restrict__ orig, const ray_pre &r,
-                                           hit_state &hs, uint32_t &roots) {
+                                           float tmin, hit_state &hs, uint32_t &roots) {
   pair_geom q[NP];
   f2 h[NP], e[NP];
   bool c[2 * NP];
@@ -400,8 +399,8 @@ __device__ __forceinline__ void scan_pairs(const RT_CONST pair_geom *__restrict_
       const int s0 = slot0 + 2 * j;
       const int i0 = orig ? orig[s0] : s0;
       const int i1 = orig ? orig[s0 + 1] : s0 + 1;
-      candidate<OPEN>(c[2 * j], h[j].x, e[j].x - q[j].ks.x, tie2_of<OPEN>((uint32_t)i0), hs);
-      candidate<OPEN>(c[2 * j + 1], h[j].y, e[j].y - q[j].ks.y, tie2_of<OPEN>((uint32_t)i1), hs);
+      candidate<OPEN>(c[2 * j], h[j].x, e[j].x - q[j].ks.x, tie2_of<OPEN>((uint32_t)i0), tmin, hs);
+      candidate<OPEN>(c[2 * j + 1], h[j].y, e[j].y - q[j].ks.y, tie2_of<OPEN>((uint32_t)i1), tmin, hs);
     }
   }
 }
@@ -421,7 +420,7 @@ __device__ __forceinline__ void scan_pairs(const RT_CONST pair_geom *__restrict_
 template <bool OPEN, bool STATS, bool LEAD>
 __device__ __forceinline__ void scan_extras(const RT_CONST pair_geom *__restrict__ g, int slot0,
                                             const RT_CONST int *__restrict__ orig, const ray_pre &r,
-                                            hit_state &hs, uint32_t &roots) {
+                                            float tmin, hit_state &hs, uint32_t &roots) {
   float h[4], d[4];
   uint32_t t[4];
   bool c[4];
@@ -447,7 +446,7 @@ __device__ __forceinline__ void scan_extras(const RT_CONST pair_geom *__restrict
   constexpr int J0 = LEAD ? 1 : 0;
   if (LEAD) {  // (candidate's own lane-mask branch skips a wave with no candidate)
     if (STATS && __builtin_amdgcn_ballot_w64(c[0])) ++roots;
-    candidate<OPEN>(c[0], h[0], d[0], t[0], hs);
+    candidate<OPEN>(c[0], h[0], d[0], t[0], tmin, hs);
   }
 #pragma unroll
   for (int round = J0; round < 4; ++round) {
@@ -471,7 +470,7 @@ __device__ __forceinline__ void scan_extras(const RT_CONST pair_geom *__restrict
     }
     if (!__builtin_amdgcn_ballot_w64(taken)) break;
     if (STATS) ++roots;
-    candidate<OPEN>(taken, hh, dd, tt, hs);
+    candidate<OPEN>(taken, hh, dd, tt, tmin, hs);
   }
 }
 
@@ -544,8 +543,8 @@ template <bool OPEN, bool STATS, bool LAYER>
 __device__ __forceinline__ int walk_step(const bvh_node &nd, int node, bool hit,
                                          const RT_CONST pair_geom *__restrict__ geom,
                                          const RT_CONST int *__restrict__ orig,
-                                         const ray_pre &rp, hit_state &hs, work_ctr &wc, float lim_src,
-                                         float &lim) {
+                                         const ray_pre &rp, float tmin, hit_state &hs, work_ctr &wc,
+                                         float lim_src, float &lim) {
   if (STATS) {
     ++wc.boxes;
     wc.box_hits += hit ? 1u : 0u;
@@ -555,10 +554,10 @@ __device__ __forceinline__ int walk_step(const bvh_node &nd, int node, bool hit,
   const int fp = (int)(nd.leaf & ~kTwoPairs) - 1;
   // a leaf of 1-2 spheres scans one pair, not a pair of padding
   if (nd.leaf & kTwoPairs) {
-    scan_pairs<OPEN, 2, STATS, LAYER>(geom + fp, 2 * fp, orig, rp, hs, wc.roots);
+    scan_pairs<OPEN, 2, STATS, LAYER>(geom + fp, 2 * fp, orig, rp, tmin, hs, wc.roots);
     if (STATS) wc.tests += 4;
   } else {
-    scan_pairs<OPEN, 1, STATS, LAYER>(geom + fp, 2 * fp, orig, rp, hs, wc.roots);
+    scan_pairs<OPEN, 1, STATS, LAYER>(geom + fp, 2 * fp, orig, rp, tmin, hs, wc.roots);
     if (STATS) wc.tests += 2;
   }
   if (LAYER) asm("v_min_f32 %0, %1, %2" : "=v"(lim) : "v"(lim_src), "v"(hs.tmax));
@@ -568,8 +567,8 @@ __device__ __forceinline__ int walk_step(const bvh_node &nd, int node, bool hit,
 // one grid item (cx, cz, ks, closed tie key): the leaf test's arithmetic in
 // plain fp32 (NOY fold: the same bits as scan_pairs) and the candidate rule
 template <bool OPEN, bool STATS>
-__device__ __forceinline__ void grid_item(const f4 it, float dx, float dz, const ray_pre &rl, hit_state &hs,
-                                          work_ctr &wc) {
+__device__ __forceinline__ void grid_item(const f4 it, float dx, float dz, const ray_pre &rl, float tmin,
+                                          hit_state &hs, work_ctr &wc) {
   if (STATS && RT_COUNT_ITEMS == 1 && lane_now() == __builtin_ctzll(__builtin_amdgcn_ballot_w64(true))) ++wc.box_hits;
   const float h = fmaf(it.y, dz, fmaf(it.x, dx, rl.nk1.x));
   const float g = fmaf(it.y, rl.oz2.x, fmaf(it.x, rl.ox2.x, rl.o2.x));
@@ -579,7 +578,7 @@ __device__ __forceinline__ void grid_item(const f4 it, float dx, float dz, const
     ++wc.box_hits;
   // it.w holds tie2_of<false>(index); the open interval's is 0xfffffffe - it
   const uint32_t w = __float_as_uint(it.w);
-  candidate<OPEN>(e >= it.z, h, e - it.z, OPEN ? 0xfffffffeu - w : w, hs);
+  candidate<OPEN>(e >= it.z, h, e - it.z, OPEN ? 0xfffffffeu - w : w, tmin, hs);
   if (STATS) ++wc.tests;
 }
 
@@ -594,7 +593,7 @@ __device__ __forceinline__ void grid_item(const f4 it, float dx, float dz, const
 // until its last lane is done.
 template <bool OPEN, bool STATS, int GP>
 __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz, float oix, float oiz,
-                                          float ta, float tb, const ray_pre &rl, hit_state &hs,
+                                          float ta, float tb, const ray_pre &rl, float tmin, hit_state &hs,
                                           work_ctr &wc) {
   const kparams p = kernargs();
   // clip to the grid's inner box (the cells around it are an empty ring);
@@ -650,7 +649,7 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
       // (both bounds behind one barrier: one wait for the two reads)
       asm volatile("" : "+v"(ip), "+v"(ie));
       if (ip != ie) do {
-        grid_item<OPEN, STATS>(*ip, dx, dz, rl, hs, wc);
+        grid_item<OPEN, STATS>(*ip, dx, dz, rl, tmin, hs, wc);
         ++ip;
       } while (ip != ie);
     } else {
@@ -669,7 +668,8 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
       uint32_t ko = k << 4;
       const uint32_t koe = ke << 4;
       if (ko != koe) do {
-        grid_item<OPEN, STATS>(*(const RT_GLOBAL f4 *)((const RT_GLOBAL char *)items + ko), dx, dz, rl, hs, wc);
+        grid_item<OPEN, STATS>(*(const RT_GLOBAL f4 *)((const RT_GLOBAL char *)items + ko), dx, dz, rl, tmin, hs,
+                               wc);
         ko += 16;
       } while (ko != koe);
     }
@@ -699,7 +699,7 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
 // bounce loop (SGPR pressure).
 template <bool OPEN, bool BVH, bool STATS, bool GRID, int GP>
 __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, float dx, float dy, float dz,
-                                                 work_ctr &wc) {
+                                                 float tmin, work_ctr &wc) {
   const kparams p = kernargs();
   const RT_CONST pair_geom *__restrict__ scan_geom = as_const(p.scan_geom);
   const RT_CONST pair_geom *__restrict__ geom = as_const(p.geom);
@@ -722,7 +722,7 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
     // brute force: 8 spheres (4 pairs) per iteration over the whole array
     const ray_pre rp = splat();
     for (int k = 0; k < n_pairs; k += 4)
-      scan_pairs<OPEN, 4, STATS>(scan_geom + k, 2 * k, nullptr, rp, hs, wc.roots);
+      scan_pairs<OPEN, 4, STATS>(scan_geom + k, 2 * k, nullptr, rp, tmin, hs, wc.roots);
     if (STATS) wc.tests += 2 * n_pairs;
   } else {
     const ray_pre rp = splat();
@@ -756,12 +756,13 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
         // (kparams extra_geom / extra_orig: the host resolved the offsets)
         const RT_CONST pair_geom *__restrict__ xg = as_const(p.extra_geom);
         const RT_CONST int *__restrict__ xo = as_const(p.extra_orig);
-        if (p.n_extra_pairs > 0) scan_extras<OPEN, STATS, true>(xg, 0, xo, rp, hs, wc.roots);
+        if (p.n_extra_pairs > 0) scan_extras<OPEN, STATS, true>(xg, 0, xo, rp, tmin, hs, wc.roots);
         for (int k = 2; k < p.n_extra_pairs; k += 2)
-          scan_extras<OPEN, STATS, false>(xg + k, 2 * k, xo, rp, hs, wc.roots);
+          scan_extras<OPEN, STATS, false>(xg + k, 2 * k, xo, rp, tmin, hs, wc.roots);
       } else {
         for (int k = 0; k < p.n_extra_pairs; k += 2)
-          scan_pairs<OPEN, 2, STATS>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, rp, hs, wc.roots);
+          scan_pairs<OPEN, 2, STATS>(geom + p.extra_pair0 + k, 2 * (p.extra_pair0 + k), orig, rp, tmin, hs,
+                                     wc.roots);
       }
       if (STATS) wc.tests += 2 * p.n_extra_pairs;
       // every node's y-range lies inside the layer's: its slab interval is
@@ -778,7 +779,7 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
         ray_pre rg = rp;  // (.x halves only: the walk is per lane)
         rg.nk1.x = fmaf(p.layer_cy, dy, nk1);
         rg.o2.x = fmaf(p.layer_cy, oy2, o2);
-        if (tyl_n <= tyl_fc) grid_walk<OPEN, STATS, GP>(ox, oz, ix, iz, oix, oiz, tyl_n, tyl_fc, rg, hs, wc);
+        if (tyl_n <= tyl_fc) grid_walk<OPEN, STATS, GP>(ox, oz, ix, iz, oix, oiz, tyl_n, tyl_fc, rg, tmin, hs, wc);
         return hs;
       }
       // a wave none of whose rays crosses the layer before tmax skips the walk
@@ -802,7 +803,7 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
         float tn, tf;
         asm("v_max3_f32 %0, %1, %2, %3" : "=v"(tn) : "v"(tn2.x), "v"(tn2.y), "v"(tyl_n));
         asm("v_min3_f32 %0, %1, %2, %3" : "=v"(tf) : "v"(tf2.x), "v"(tf2.y), "v"(tyl_fc));
-        node = walk_step<OPEN, STATS, true>(nd, node, tn <= tf, geom, orig, rl, hs, wc, tyl_f, tyl_fc);
+        node = walk_step<OPEN, STATS, true>(nd, node, tn <= tf, geom, orig, rl, tmin, hs, wc, tyl_f, tyl_fc);
       }
     } else if (!GRID) {  // (the grid build runs on layer scenes only)
       const f2 vix = {ix, ix}, viy = {iy, iy}, viz = {iz, iz};
@@ -816,7 +817,7 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
         const float tn = fmaxf(fmaxf(fmaxf(fminf(tx.x, tx.y), fminf(ty.x, ty.y)), fminf(tz.x, tz.y)), 0.0f);
         const float tf = fminf(fminf(fminf(fmaxf(tx.x, tx.y), fmaxf(ty.x, ty.y)), fmaxf(tz.x, tz.y)), hs.tmax);
         float unused = 0.0f;
-        node = walk_step<OPEN, STATS, false>(nd, node, tn <= tf, geom, orig, rp, hs, wc, 0.0f, unused);
+        node = walk_step<OPEN, STATS, false>(nd, node, tn <= tf, geom, orig, rp, tmin, hs, wc, 0.0f, unused);
       }
     }
   }
@@ -899,6 +900,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
     __syncthreads();
   }
   float ox = 0.f, oy = 0.f, oz = 0.f, dx = 0.f, dy = 1.f, dz = 0.f;
+  float tmin = 0.001f;  // the ray's t_min (normalize3: 0.001 |d| of its unnormalised direction)
   float thr = 1.f, thg = 1.f, thb = 1.f;
   int depth = 0;
   uint32_t slot = 0, sample = 0, pix = 0;
@@ -932,7 +934,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
     if (tracing) {
       int col, grow;
       pixel_cr(p, col, grow);
-      camera_ray(p, pcg4d(pix, sample, 0u, p.seed32), col, grow, ox, oy, oz, dx, dy, dz);
+      tmin = camera_ray(p, pcg4d(pix, sample, 0u, p.seed32), col, grow, ox, oy, oz, dx, dy, dz);
     }
   }
 
@@ -941,7 +943,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   // wave-level any-alive ballot per step)
   while (alive) {
     hit_state hs = no_hit();
-    if (tracing) hs = closest_hit<OPEN, BVH, STATS, GRID, GP>(ox, oy, oz, dx, dy, dz, wc);
+    if (tracing) hs = closest_hit<OPEN, BVH, STATS, GRID, GP>(ox, oy, oz, dx, dy, dz, tmin, wc);
     ++steps;
     const int best = best_of<OPEN>(hs);
     // lanes that end their path here (a miss) or hold a slot outside the frame
@@ -954,6 +956,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
       knext += (uint32_t)__builtin_popcountll(need);
     }
     bool path_done = false;  // absorbed, or the bounce limit: the lane parks for a step
+    bool skipped = false;    // a spurious root: same ray from further along, same t_min
     {
       const kparams q = kernargs();  // shading's parameters, re-read per step
       if (tracing) ++segs;
@@ -1015,11 +1018,12 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         // (b > 0): the ray starts on that sphere and leaves its ball, which it
         // cannot meet again; the expanded quadratic's root was an fp32 artefact
         // (DESIGN.md 2, step 3).  Not a segment: the ray moves on to the
-        // scan's root point, same direction, and walks again.
-        if (t < 0.001f && b > 0.0f) {
+        // scan's root point, same direction (and t_min), and walks again.
+        if (t < tmin && b > 0.0f) {
           ox = fmaf(tmax, dx, ox);
           oy = fmaf(tmax, dy, oy);
           oz = fmaf(tmax, dz, oz);
+          skipped = true;
           --segs;
         } else {
         const float px = fmaf(t, dx, ox), py = fmaf(t, dy, oy), pz = fmaf(t, dz, oz);
@@ -1119,8 +1123,10 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
     // (one camera-ray path per step, with the step's one hash)
     if (path_done) tracing = false;
     // one normalize3 per lane and step: the bounce direction or the new
-    // camera ray's (a finished lane's is unused)
-    normalize3(dx, dy, dz);
+    // camera ray's (a finished lane's is unused), and with it the ray's t_min
+    // (a skipped ray keeps its own)
+    const float tmin_new = normalize3(dx, dy, dz);
+    tmin = skipped ? tmin : tmin_new;
   }
 
   const int lane = lane_now();
@@ -1202,7 +1208,7 @@ __global__ __launch_bounds__(256) void finish_sums_wide(const uint64_t *__restri
 // (rt_device_kat; tests/test_parity_gpu.py checks it against the reference's
 // vectors in tests/golden/kat.jsonl).  Case layout: 10 doubles in, 9 out.
 //   RT_KAT_SPHERE_HIT  in  o[3] d[3] c[3] r      (sphere::hit, src/cpu/sphere.h:24-51,
-//                                                  t_min 0.001, t_max inf)
+//                                                  t_min 0.001 in units of d, t_max inf)
 //                      out hit, t (in units of the given d), p[3], normal[3], front_face
 //                      -- the scan's candidate test, refine_root, the shading normal
 //                      and set_face_normal, exactly as render_kernel runs them on a
@@ -1221,7 +1227,7 @@ __global__ __launch_bounds__(64) void kat_kernel(int kind, const double *__restr
     const float ox = (float)a[0], oy = (float)a[1], oz = (float)a[2];
     float dx = (float)a[3], dy = (float)a[4], dz = (float)a[5];
     const double len = sqrt(a[3] * a[3] + a[4] * a[4] + a[5] * a[5]);
-    normalize3(dx, dy, dz);
+    const float tmin = normalize3(dx, dy, dz);
     shade_rec sr;
     sr.cx = (float)a[6];
     sr.cy = (float)a[7];
@@ -1237,7 +1243,7 @@ __global__ __launch_bounds__(64) void kat_kernel(int kind, const double *__restr
     const float g = fmaf(sr.cz, oz2, fmaf(sr.cx, ox2, fmaf(sr.cy, oy2, o2)));
     const float e = fmaf(h, h, -g);
     hit_state hs = no_hit();
-    candidate<false>(e >= sr.ks, h, e - sr.ks, tie2_of<false>(0u), hs);
+    candidate<false>(e >= sr.ks, h, e - sr.ks, tie2_of<false>(0u), tmin, hs);
     if (best_of<false>(hs) < 0) return;
     float b_unused;
     const float t = refine_root(sr, hs.tmax, near_of(hs) != 0, ox, oy, oz, dx, dy, dz, o2, ox2, oy2, oz2, b_unused);

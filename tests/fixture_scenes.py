@@ -58,7 +58,39 @@ def hot_scene(rtow):
     ])
 
 
-FIXTURES = {"embed": embedded_glass_scene, "negop": negative_opaque_scene, "hot": hot_scene}
+def _resting(x, z, r):
+    """Centre of a sphere of radius r resting on the r = 1000 ground at (x, z):
+    |C - (0, -1000, 0)| = 1000 + r (in fp64; the fp32 centre is within an ulp)."""
+    return (x, -1000.0 + float(np.sqrt((1000.0 + r) ** 2 - x * x - z * z)), z)
+
+
+def contact_scene(rtow):
+    """Contacts, where the reference's t_min unit matters:
+    small lambertian and metal spheres resting on the lambertian ground (r =
+    0.05-0.3), two lambertian balls touching each other, and a lambertian ball
+    touching a glass one, all in the view of the file-scene camera ((13, 2, 3)
+    -> 0, 8.5 degrees above the ground).  A ray scattered off the ground next
+    to a contact meets the other surface within a few t_min: the reference
+    tests that root against 0.001 |d| (|d| = 2 cos theta for a lambertian
+    bounce), the round-4 specification against 0.001 world units."""
+    rows = [(0.0, -1000.0, 0.0, 1000.0, 0, (0.5, 0.5, 0.5), 0.0)]
+    small = [(1.6, 0.9, 0.05, 0, (0.8, 0.3, 0.3), 0.0), (1.9, 0.5, 0.1, 0, (0.3, 0.8, 0.3), 0.0),
+             (2.4, -0.2, 0.2, 0, (0.3, 0.3, 0.8), 0.0), (1.2, -1.1, 0.3, 0, (0.8, 0.8, 0.3), 0.0),
+             (2.8, 1.3, 0.15, 1, (0.8, 0.8, 0.8), 0.0), (0.6, 1.6, 0.25, 1, (0.7, 0.6, 0.5), 0.4),
+             (3.2, -1.0, 0.1, 1, (0.9, 0.9, 0.9), 0.1)]
+    for x, z, r, kind, alb, param in small:
+        rows.append(_resting(x, z, r) + (r, kind, alb, param))
+    # two lambertian balls touching each other, both on the ground
+    rows.append(_resting(-0.4, 1.4, 0.35) + (0.35, 0, (0.6, 0.5, 0.3), 0.0))
+    rows.append(_resting(-0.4, 2.1, 0.35) + (0.35, 0, (0.3, 0.5, 0.6), 0.0))
+    # a lambertian ball touching a glass ball
+    rows.append(_resting(-0.6, -1.0, 0.5) + (0.5, 0, (0.7, 0.7, 0.7), 0.0))
+    rows.append(_resting(-0.6, -2.0, 0.5) + (0.5, 2, (1.0, 1.0, 1.0), 1.5))
+    return _scene(rtow, rows)
+
+
+FIXTURES = {"embed": embedded_glass_scene, "negop": negative_opaque_scene, "hot": hot_scene,
+            "contact": contact_scene}
 
 
 # Segment counts: over 12 oracle seeds the relative deviation from the

@@ -69,9 +69,19 @@ def reference_render_view(scene, width, aspect, spp, max_depth=50):
     return out, seg.value
 
 
-def kernel_render(scene, cam, params, threads=0):
-    """fp32 restatement of the kernel algorithm -> (float32 [rows, W, 3], segments)."""
-    import rtow
+# rto_kernel_render_exact's opts bits (oracle/rt_oracle.h): superseded forms
+# of the specification, for the tests that show why they changed
+RTO_OPT_NO_DITHER = 1
+RTO_OPT_TMIN_WORLD = 2
+
+
+def kernel_render(scene, cam, params, threads=0, tmin_world=False):
+    """fp32 restatement of the kernel algorithm -> (float32 [rows, W, 3], segments).
+    tmin_world: t_min 0.001 in world units on the normalised ray (the
+    round-1..4 specification) instead of the reference's unit, 0.001 |d|."""
+    if tmin_world:
+        out, _, segs = _kernel_render_opts(scene, cam, params, RTO_OPT_TMIN_WORLD, False, threads)
+        return out, segs
     v = scene.view()
     out = np.zeros((params.local_rows, params.width, 3), np.float32)
     seg = ctypes.c_ulonglong()
@@ -80,22 +90,26 @@ def kernel_render(scene, cam, params, threads=0):
     return out, seg.value
 
 
-def kernel_render_exact(scene, cam, params, no_dither=False, threads=0):
-    """kernel_render plus each pixel's fp64 sum of the unquantised sample
-    radiances (the reference's fp64 accumulation, src/cpu/main.cc:114-119, of
-    the same samples) -> (float32 sums, float64 exact sums, segments).
-    no_dither: the sum format without stochastic rounding (truncation)."""
+def _kernel_render_opts(scene, cam, params, opts, want_exact, threads):
     v = scene.view()
     out = np.zeros((params.local_rows, params.width, 3), np.float32)
-    exact = np.zeros((params.local_rows, params.width, 3), np.float64)
+    exact = np.zeros((params.local_rows, params.width, 3), np.float64) if want_exact else None
     seg = ctypes.c_ulonglong()
     L = lib()
     L.rto_kernel_render_exact.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_int, ctypes.POINTER(ctypes.c_ulonglong),
                                                                    ctypes.c_int]
     assert L.rto_kernel_render_exact(ctypes.addressof(v), ctypes.addressof(cam), ctypes.addressof(params),
-                                     out.ctypes.data, exact.ctypes.data, int(no_dither), ctypes.byref(seg),
-                                     threads) == 0
+                                     out.ctypes.data, exact.ctypes.data if want_exact else None, int(opts),
+                                     ctypes.byref(seg), threads) == 0
     return out, exact, seg.value
+
+
+def kernel_render_exact(scene, cam, params, no_dither=False, threads=0):
+    """kernel_render plus each pixel's fp64 sum of the unquantised sample
+    radiances (the reference's fp64 accumulation, src/cpu/main.cc:114-119, of
+    the same samples) -> (float32 sums, float64 exact sums, segments).
+    no_dither: the sum format without stochastic rounding (truncation)."""
+    return _kernel_render_opts(scene, cam, params, RTO_OPT_NO_DITHER if no_dither else 0, True, threads)
 
 
 def trace(scene, cam, params, col, row, sample, max_depth=50):

@@ -282,9 +282,9 @@ def _hit_cases():
 def _ambiguous(k):
     """True where an fp32 evaluation may legitimately differ from the
     reference's fp64 sphere::hit: a near-zero discriminant (grazing: hit flag
-    and face undecided), or a root within reach of t_min -- the reference's
-    t_min is 0.001 in units of its unnormalised direction, the kernel's 0.001
-    in distance (its directions are normalised)."""
+    and face undecided), or a root within fp32 reach of t_min (0.001 in units
+    of the unnormalised direction, in the reference and, since round 5, in the
+    kernel: normalize3 returns 0.001 |d|)."""
     o, d, c = (np.array(k[x], np.float64) for x in ("o", "d", "c"))
     r = float(k["r"])
     oc = o - c
@@ -296,10 +296,8 @@ def _ambiguous(k):
     if disc < 0:
         return False
     L = np.sqrt(a)
-    lo, hi = 0.001 * min(1.0, L), 0.001 * max(1.0, L)
     for t in ((-hb - np.sqrt(disc)) / a, (-hb + np.sqrt(disc)) / a):
-        dist = t * L  # distance along the ray
-        if lo - 1e-4 <= dist <= hi + 1e-4:
+        if abs(t - 0.001) * L <= 1e-4:  # distance along the ray from the t_min point
             return True
     return False
 
@@ -333,7 +331,8 @@ def test_device_sphere_hit_random_kat(rtow, gpu_ctx):
         en = float(np.abs(np.array(o[5:8]) - k["normal"]).max()) * abs(k["r"]) / scale
         worst = [max(worst[0], et), max(worst[1], ep), max(worst[2], en)]
     print("checked", checked, "hits", hits, "worst (t, p, normal*r) / scale", worst)
-    assert checked >= 500 and hits >= 250
+    # 585 of 600 decidable (584 with the round-4 world-unit t_min window)
+    assert checked >= 585 and hits >= 250
     # measured: 4.7e-7, 3.1e-7, 3.2e-7 (profiles/r03ad_hit_kat.log)
     assert worst[0] <= 1e-6 and worst[1] <= 1e-6 and worst[2] <= 1e-6, worst
 
@@ -362,7 +361,7 @@ def test_device_reflect_refract_reflectance_random_kat(rtow, gpu_ctx):
     assert e_rf <= 1e-6 and e_rr <= 2e-6 and e_sc <= 1e-6, (e_rf, e_rr, e_sc)
 
 
-@pytest.mark.parametrize("key", ["embed", "negop", "hot"])
+@pytest.mark.parametrize("key", ["embed", "negop", "hot", "contact"])
 def test_rule_and_albedo_fixtures_vs_reference(rtow, gpu_ctx, key):
     """The opaque-inside rule's reference fixtures (tests/fixture_scenes.py,
     src/cpu through ref_harness file:, 320x180 @ 256 spp): a glass sphere

@@ -1,10 +1,15 @@
 #!/bin/bash
-# Run GPU steps in order, each under its own time limit.  A step that fails
-# normally (exit 1: a test failure) does not stop the sequence; a crash,
-# abort, fault or time-out (anything else non-zero) ends it -- nothing more
-# touches the GPU after that.
+# The one runner of every GPU session (round 5: the per-session scripts of
+# rounds 3-4 are gone).  Runs GPU steps in order, each under its own time
+# limit.  A step that fails normally (exit 1: a test failure) does not stop
+# the sequence; a crash, abort, fault or time-out (anything else non-zero) ends
+# it -- nothing more touches the GPU after that.
 #   tools/gpu_steps.sh "name|seconds|command" ...
+# The argument list is written to gpurun_out/<first step>.steps, which is
+# committed under profiles/ with the logs it produced.
 mkdir -p gpurun_out
+first="${1%%|*}"
+printf '%s\n' "$@" > "gpurun_out/$first.steps"
 for spec in "$@"; do
   name="${spec%%|*}"; rest="${spec#*|}"; secs="${rest%%|*}"; cmd="${rest#*|}"
   echo "== $name (limit ${secs}s): $cmd"
