@@ -84,9 +84,6 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pilot", action="store_true",
                     help="launch tiles in index order (no RT_FLAG_PILOT_SCHEDULE)")
-    ap.add_argument("--grid-tune", action="store_true",
-                    help="pick the layer grid's cell size by rt_tune_grid's pilots before the warmup "
-                         "(opt-in: its picks do not reliably carry over to the full frame, DESIGN 3.3)")
     ap.add_argument("--out", default="", help="write the gathered frame as PPM (P6 if .pgm/.p6)")
     a = ap.parse_args()
     if a.preset:
@@ -271,21 +268,6 @@ def main():
         params.flags |= rtow.RT_FLAG_ACCEL_BVH
     if a.accel == "layer_bvh":
         params.flags |= rtow.RT_FLAG_LAYER_BVH
-    # --grid-tune: the layer grid's cell size for this frame geometry
-    # (rt_tune_grid: pilots per candidate, before the warmup; the image is the
-    # same for every candidate)
-    grid_tune = None
-    if a.accel == "bvh" and a.grid_tune:
-        t_tune = time.perf_counter()
-        g = ctx.tune_grid(cam, params)
-        cands = ctx.grid_candidates()
-        base_ms = cands[0][1] if cands else None
-        kept_ms = next((m for s_, m in cands if abs(s_ - g) < 1e-9), None)
-        grid_tune = {"cell_scale": round(g, 4), "candidates": len(cands),
-                     "pilot_ms_builder_grid": round(base_ms, 4) if base_ms is not None else None,
-                     "pilot_ms_kept_grid": round(kept_ms, 4) if kept_ms is not None else None,
-                     "pilot_ms": {f"{s_:.4f}": round(m, 4) for s_, m in cands},
-                     "wall_ms": round((time.perf_counter() - t_tune) * 1e3, 1)}
     tile = torch.zeros((params.local_rows, W, 3), dtype=torch.float32, device=dev)
     # the step ends like the drop-in CLI's: write_color on the device (src/cpu
     # arithmetic) turns the tile's sums into bytes, and rank 0 gathers the byte
@@ -426,7 +408,6 @@ def main():
             "work_per_launch_rank0": {"segments": work.segments, "sphere_tests": work.sphere_tests,
                                       "box_tests": work.box_tests, "box_hits_own_ray": work.box_hits,
                                       "brute_force_equiv_tests": work.bf_tests},
-            "grid_tune": grid_tune,
             "first_frame_ms": round(first_frame_ms, 3) if first_frame_ms is not None else None,
             "first_frame_note": "wall time of the first frame of this geometry on its own, pilot schedule "
                                 "included (4-spp pilot + device sort of the tile order); ms_per_step "

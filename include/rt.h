@@ -29,7 +29,9 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+/* 5: rt_tune_grid and rt_internal_grid_candidates removed, RT_ACCEL_INFO_N 18,
+ * t_min in units of the unnormalised direction (round 5) */
+#define RT_ABI_VERSION 5
 
 typedef enum {
   RT_OK = 0,
@@ -286,25 +288,6 @@ int rt_render_async(rt_context *ctx, const rt_camera *cam, const rt_params *para
 int rt_render(rt_context *ctx, const rt_camera *cam, const rt_params *params,
               float *host_rgb, rt_stats *stats);
 
-/* Layer-grid cell size for this frame geometry (scheduling only: every
- * candidate renders the same image).  A scene whose layer grid sits in LDS
- * (RT_GRID_LDS or RT_GRID_CELLS_LDS) is uploaded with candidate grids of cell
- * scale s0 (1 + 0.01 k), k = 0..30, each fitting the same placement (s0 = the
- * RT_OPT_GRID_SCALE grid).  Where the cell borders fall relative to the
- * spheres the frame's rays meet most moves the walk's cost by several per
- * cent, so this renders a short pilot of (cam, params) --
- * min(spp, 128) samples per pixel on a uniform subset of the tiles, about
- * 2^27 samples, into a context-owned buffer -- three times with every candidate,
- * keeps the fastest for
- * the context's following renders and stores its scale in *grid_scale (may
- * be NULL; 0 without a grid).  Synchronous; waits for the device first.
- * RT_OK without rendering when there is nothing to choose (no candidates,
- * no RT_FLAG_ACCEL_BVH or RT_FLAG_LAYER_BVH, nothing traced).  The kept
- * candidate must beat the builder's grid by 1 %, else that one stays.  A new rt_scene_upload starts again
- * from s0.  Not in the reference (its one kernel has no acceleration
- * structure to tune). */
-int rt_tune_grid(rt_context *ctx, const rt_camera *cam, const rt_params *params, double *grid_scale);
-
 /* Progress of the last rt_render_async / rt_render of this context, without
  * blocking: how many of its bounded launches (RT_OPT_LAUNCH_SAMPLES) have
  * completed, of how many.  RT_ERR_HIP if the device reported a fault in one
@@ -372,10 +355,8 @@ int rt_device_kat(int device, int kind, const double *in, size_t n_cases, double
  *   8 grid LDS bytes        9 whole grid in LDS 10 max items/cell 11 start invariant
  *  12 empty ring cells ok  13 oref * 1000      14 layer slots    15 listed cells
  *  16 placement (RT_GRID_*, 0: no grid)         17 cell scale * 1000
- *  18 candidate grids of rt_tune_grid (0: none)
- *  19 every candidate keeps 11 and 12 and fits the placement's LDS budget
  * For tests and sanitizer runs. */
-#define RT_ACCEL_INFO_N 20
+#define RT_ACCEL_INFO_N 18
 int rt_internal_accel_info(const rt_scene_view *scene, int grid_placement, double grid_scale, uint64_t *out,
                            size_t n_out);
 
@@ -387,11 +368,6 @@ int rt_internal_accel_info(const rt_scene_view *scene, int grid_placement, doubl
  * For tests. */
 #define RT_LAUNCH_PLAN_N 5
 int rt_internal_launch_plan(const rt_params *params, double launch_samples, uint64_t *out, size_t n_out);
-
-/* The context's candidate grids (rt_tune_grid): *n = their count; for the
- * first min(n_out, *n), the cell scale and the last rt_tune_grid's pilot
- * time in ms (NaN before one ran).  For tests and the bench record. */
-int rt_internal_grid_candidates(rt_context *ctx, double *scales, float *ms, size_t n_out, size_t *n);
 
 /* Host only (no device): for each sphere of `scene`, 1 if the kernel's
  * opaque-inside rule applies to it (a sealed lambertian sphere: no other

@@ -58,7 +58,6 @@ struct options {
   std::string gather = "auto";  // auto: rccl when gpus > 1
   std::string out;
   bool p6 = false, quiet = false;
-  bool tune_grid = false;  // --tune-grid: rt_tune_grid before the render (pays over many frames, not one)
 };
 
 [[noreturn]] void die(const char *what, int st) {
@@ -75,8 +74,7 @@ void check(int st, const char *what) {
                "usage: %s [--width N] [--height N] [--spp N] [--depth N] [--seed N]\n"
                "          [--spheres HALF_EXTENT] [--scene final|five] [--camera cpu|gpu]\n"
                "          [--semantics cpu|gpu] [--accel bvh|scan] [--gpus N] [--device N]\n"
-               "          [--devices D0,D1,...] [--gather rccl|host] [--out FILE] [--p6] [--quiet]\n"
-               "          [--tune-grid]\n",
+               "          [--devices D0,D1,...] [--gather rccl|host] [--out FILE] [--p6] [--quiet]\n",
                argv0);
   std::exit(2);
 }
@@ -133,7 +131,6 @@ int main(int argc, char **argv) {
     else if (a == "--out") o.out = next();
     else if (a == "--p6") o.p6 = true;
     else if (a == "--quiet") o.quiet = true;
-    else if (a == "--tune-grid") o.tune_grid = true;
     else usage(argv[0]);
   }
   if (!height_set && (o.width != (gpu_mode ? 1920 : 1200))) {
@@ -240,9 +237,6 @@ int main(int argc, char **argv) {
   for (int g = 0; g < o.gpus; ++g) {
     check(rt_context_create(jobs[g].device, &ctxs[g]), "rt_context_create");
     check(rt_scene_upload(ctxs[g], &view), "rt_scene_upload");
-    // --tune-grid: the layer grid's cell size for this device's share
-    // (scheduling only; its pilots cost a good part of one frame, so not by default)
-    if (o.tune_grid) check(rt_tune_grid(ctxs[g], &cam, &jobs[g].params, nullptr), "rt_tune_grid");
   }
   const bool use_rccl = o.gather == "rccl" || (o.gather == "auto" && o.gpus > 1);
   // Every device renders its tile (fp32 sums) and tonemaps it on the device

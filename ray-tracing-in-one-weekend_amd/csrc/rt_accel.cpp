@@ -588,37 +588,6 @@ void build_accel(const rt_scene_view *s, const accel_options &o, accel_build &a)
   a.grid_nz = bb.grid_nz;
   a.grid_scale = bb.grid_scale;
   a.grid_placement = bb.grid_cells.empty() ? kGridGlobal : place;
-  // the candidates for rt_tune_grid: coarser cells that fit the same placement
-  // (every one renders the same image: the lists hold every sphere that can win)
-  if (a.grid_placement == kGridLds || a.grid_placement == kGridCells) {
-    const auto snap = [&] {
-      grid_geom q;
-      q.cells = bb.grid_cells;
-      q.items = bb.grid_items;
-      q.x0 = bb.grid_x0;
-      q.z0 = bb.grid_z0;
-      q.xi = bb.grid_xi;
-      q.zi = bb.grid_zi;
-      q.x1 = bb.grid_x1;
-      q.z1 = bb.grid_z1;
-      q.g = bb.grid_g;
-      q.nx = bb.grid_nx;
-      q.nz = bb.grid_nz;
-      q.scale = bb.grid_scale;
-      return q;
-    };
-    a.grid_alts.push_back(snap());
-    const double s0 = bb.grid_scale;
-    for (int k = 1; k <= kGridTuneSteps; ++k) {
-      bb.grid_scale = s0 * (1.0 + kGridTuneStep * k);
-      bb.build_grid(s, bb.n_layer);
-      if (bb.grid_cells.empty()) continue;
-      const bool fits = a.grid_placement == kGridLds
-                            ? n_items() < 4096 && grid_lds_bytes(kGridLds, n_items(), n_cells()) <= lds_max
-                            : n_items() < 65536 && grid_lds_bytes(kGridCells, n_items(), n_cells()) <= lds_max;
-      if (fits) a.grid_alts.push_back(snap());
-    }
-  }
 }
 
 }  // namespace rtk

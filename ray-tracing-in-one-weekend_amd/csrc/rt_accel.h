@@ -23,23 +23,6 @@ struct accel_options {
   bool wide = false;         // 64-bit pixel sums (an albedo above 1): less LDS for the grid
 };
 
-// one layer grid: cells (first item << 4 | count, row-major with the empty
-// ring), items (cx, cz, ks, tie key) and its geometry
-struct grid_geom {
-  std::vector<uint32_t> cells;
-  std::vector<float> items;  // 4 floats per item
-  float x0 = 0, z0 = 0, xi = 0, zi = 0, x1 = 0, z1 = 0, g = 0;
-  int nx = 0, nz = 0;
-  double scale = 1.0;
-};
-
-// Candidate cell sizes for rt_tune_grid: the grid at scale s0 (the chosen
-// one) and at s0 (1 + k kGridTuneStep), k = 1..kGridTuneSteps, that fit the
-// same placement.  Which one walks fastest depends on where the cell borders
-// fall relative to the spheres the frame's rays meet most, so it is measured.
-constexpr int kGridTuneSteps = 30;
-constexpr double kGridTuneStep = 0.01;
-
 // everything rt_scene_upload copies to the device, plus the builder's facts
 struct accel_build {
   uint32_t n = 0, n_pad = 0;
@@ -60,8 +43,6 @@ struct accel_build {
   int grid_nx = 0, grid_nz = 0;
   double grid_scale = 1.0;        // the cell scale the grid was built with
   int grid_placement = kGridGlobal;
-  // kGridLds / kGridCells: the candidate grids, [0] = the grid above
-  std::vector<grid_geom> grid_alts;
 };
 
 // arrays present, known materials, finite centres and radii, non-zero radii,

@@ -47,19 +47,6 @@ struct rt_context {
   float grid_x0 = 0, grid_z0 = 0, grid_xi = 0, grid_zi = 0, grid_x1 = 0, grid_z1 = 0, grid_g = 0;
   int grid_nx = 0, grid_nz = 0;
   double grid_scale = 1.0;
-  // the candidate grids of rt_tune_grid (empty: only the grid above); the
-  // fields above are a copy of grid_alts[grid_cur]
-  struct grid_dev {
-    uint32_t *cells = nullptr;
-    float *items = nullptr;
-    size_t n_items = 0;
-    float x0 = 0, z0 = 0, xi = 0, zi = 0, x1 = 0, z1 = 0, g = 0;
-    int nx = 0, nz = 0;
-    double scale = 1.0;
-  };
-  std::vector<grid_dev> grid_alts;
-  size_t grid_cur = 0;
-  std::vector<float> tune_ms;  // the last rt_tune_grid's pilot times per candidate
   unsigned long long *d_counters = nullptr;
   float *d_frame = nullptr;
   size_t frame_floats = 0;
@@ -143,17 +130,8 @@ void free_scene(rt_context *c) {
   (void)hipFree(c->d_nodes);
   (void)hipFree(c->d_orig);
   (void)hipFree(c->d_shade);
-  if (c->grid_alts.empty()) {
-    (void)hipFree(c->d_grid_cells);
-    (void)hipFree(c->d_grid_items);
-  }
-  for (const rt_context::grid_dev &g : c->grid_alts) {  // the current grid is one of them
-    (void)hipFree(g.cells);
-    (void)hipFree(g.items);
-  }
-  c->grid_alts.clear();
-  c->grid_cur = 0;
-  c->tune_ms.clear();
+  (void)hipFree(c->d_grid_cells);
+  (void)hipFree(c->d_grid_items);
   c->d_grid_cells = nullptr;
   c->d_grid_items = nullptr;
   c->grid_nx = c->grid_nz = 0;
@@ -176,25 +154,6 @@ hipError_t upload_vec(T **dst, const std::vector<T> &v, hipStream_t st) {
   if (e == hipSuccess && !v.empty())
     e = hipMemcpyAsync(*dst, v.data(), sizeof(T) * v.size(), hipMemcpyHostToDevice, st);
   return e;
-}
-
-// make candidate grid j the one renders walk (rt_tune_grid)
-void select_grid(rt_context *c, size_t j) {
-  const rt_context::grid_dev &g = c->grid_alts[j];
-  c->grid_cur = j;
-  c->d_grid_cells = g.cells;
-  c->d_grid_items = g.items;
-  c->grid_n_items = g.n_items;
-  c->grid_x0 = g.x0;
-  c->grid_z0 = g.z0;
-  c->grid_xi = g.xi;
-  c->grid_zi = g.zi;
-  c->grid_x1 = g.x1;
-  c->grid_z1 = g.z1;
-  c->grid_g = g.g;
-  c->grid_nx = g.nx;
-  c->grid_nz = g.nz;
-  c->grid_scale = g.scale;
 }
 
 // F = 31 - floor(log2(spp)): spp samples of at most 2^F each fit a uint32
@@ -354,34 +313,10 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
   if (e == hipSuccess) e = upload_vec(&c->d_nodes, a.nodes, c->stream);
   if (e == hipSuccess) e = upload_vec(&c->d_orig, a.slots, c->stream);
   if (e == hipSuccess) e = upload_vec(&c->d_shade, a.shade, c->stream);
-  if (e == hipSuccess && !a.grid_cells.empty() && a.grid_alts.empty()) {
+  if (e == hipSuccess && !a.grid_cells.empty()) {
     e = upload_vec(&c->d_grid_cells, a.grid_cells, c->stream);
     if (e == hipSuccess) e = upload_vec(&c->d_grid_items, a.grid_items, c->stream);
     c->grid_n_items = a.grid_items.size() / 4;
-    c->grid_placement = a.grid_placement;
-  }
-  // candidate grids (rt_tune_grid): all on the device, [0] = the builder's
-  for (size_t j = 0; e == hipSuccess && j < a.grid_alts.size(); ++j) {
-    const rtk::grid_geom &q = a.grid_alts[j];
-    rt_context::grid_dev g;
-    e = upload_vec(&g.cells, q.cells, c->stream);
-    if (e == hipSuccess) {
-      e = upload_vec(&g.items, q.items, c->stream);
-      if (e != hipSuccess) (void)hipFree(g.cells);
-    }
-    if (e != hipSuccess) break;
-    g.n_items = q.items.size() / 4;
-    g.x0 = q.x0;
-    g.z0 = q.z0;
-    g.xi = q.xi;
-    g.zi = q.zi;
-    g.x1 = q.x1;
-    g.z1 = q.z1;
-    g.g = q.g;
-    g.nx = q.nx;
-    g.nz = q.nz;
-    g.scale = q.scale;
-    c->grid_alts.push_back(g);
     c->grid_placement = a.grid_placement;
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -411,7 +346,6 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
   c->grid_nx = a.grid_nx;
   c->grid_nz = a.grid_nz;
   c->grid_scale = a.grid_scale;
-  if (!c->grid_alts.empty()) select_grid(c, 0);
   return RT_OK;
 }
 
@@ -731,8 +665,8 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
   return RT_OK;
 }
 
-// rt_render's and rt_tune_grid's frame buffer (only they use d_frame, and
-// they return after their work is done)
+// rt_render's frame buffer (only it uses d_frame, and it returns after its
+// work is done)
 hipError_t ensure_frame(rt_context *c, size_t nf) {
   if (nf <= c->frame_floats) return hipSuccess;
   (void)hipFree(c->d_frame);
@@ -841,112 +775,6 @@ int rt_internal_launch_plan(const rt_params *prm, double launch_samples, uint64_
   return RT_OK;
 }
 
-int rt_tune_grid(rt_context *c, const rt_camera *cam, const rt_params *prm, double *scale_out) {
-  if (!c || !cam || !params_ok(prm)) return RT_ERR_INVALID;
-  if (cam->model != RT_CAMERA_CPU && cam->model != RT_CAMERA_GPU) return RT_ERR_INVALID;
-  if (cam->model == RT_CAMERA_CPU && (prm->width < 2 || prm->height < 2)) return RT_ERR_INVALID;
-  if (!c->d_geom) return RT_ERR_NO_SCENE;
-  if (scale_out) *scale_out = c->d_grid_cells ? c->grid_scale : 0.0;
-  const uint64_t px = (uint64_t)prm->width * valid_rows(prm);
-  if (c->grid_alts.size() < 2 || prm->spp <= 0 || prm->max_depth <= 0 || px == 0 ||
-      !(prm->flags & RT_FLAG_ACCEL_BVH) || (prm->flags & RT_FLAG_LAYER_BVH))
-    return RT_OK;
-  RT_HIP(hipSetDevice(c->device));
-  // renders on any stream may still walk the current grid
-  RT_HIP(hipDeviceSynchronize());
-  RT_HIP(ensure_frame(c, 3 * (size_t)prm->width * (size_t)prm->local_rows));
-  // the render's own variant (placement, sum format), one unit, float stores,
-  // launch order.  Each block gets about the samples per pixel of a render
-  // (min(spp, 128)), over every S-th block (a uniform subset of the tiles) so
-  // that a candidate's pilot stays near 2^27 samples: with a few samples per
-  // pixel over all tiles, each block's copy of the grid into LDS would weigh
-  // far more than in the render and favour the coarsest grid.
-  rtk::kparams kp;
-  fill_kparams(c, cam, prm, c->d_frame, kp);
-  const sum_fmt fmt = sum_format(prm->spp, prm->max_depth, c->max_albedo);
-  const int v = render_variant(c, prm, fmt.wide) & ~rtk::kVarStats;
-  kp.qscale = std::ldexp(1.0f, fmt.f);
-  kp.qinv = std::ldexp(1.0f, -fmt.f);
-  kp.vcap = fmt.vcap;
-  kp.dither = fmt.f < 20 ? 1 : 0;
-  kp.units = 1;
-  kp.sum_atomic = 0;
-  kp.s_lo = 0;
-  kp.s_cnt = std::min(prm->spp, 128);
-  const int tiles_y = (prm->local_rows + rtk::kTile - 1) / rtk::kTile;
-  const long long tiles = (long long)kp.tiles_x * tiles_y;
-  const long long all_blocks = (tiles + rtk::kWavesPerBlock - 1) / rtk::kWavesPerBlock;
-  const long long stride =
-      std::max<long long>(1, std::llround((double)px * kp.s_cnt / (double)(1 << 27)));
-  kp.block_stride = (int)std::min<long long>(stride, all_blocks);
-  kp.block_base = kp.block_stride / 2;
-  const unsigned blocks = (unsigned)((all_blocks - kp.block_base + kp.block_stride - 1) / kp.block_stride);
-  const size_t n = c->grid_alts.size();
-  constexpr int kPasses = 3;
-  // scratch counters and timing events, released on every path
-  struct scratch {
-    unsigned long long *ctr = nullptr;
-    std::vector<hipEvent_t> ev;
-    ~scratch() {
-      for (hipEvent_t e : ev) (void)hipEventDestroy(e);
-      (void)hipFree(ctr);
-    }
-  } sc;
-  RT_HIP(hipMalloc(&sc.ctr, 8 * rtk::kCounterSlots * sizeof(unsigned long long)));
-  RT_HIP(hipMemset(sc.ctr, 0, 8 * rtk::kCounterSlots * sizeof(unsigned long long)));
-  kp.counters = sc.ctr;
-  for (size_t k = 0; k < 2 * n * kPasses; ++k) {
-    hipEvent_t e = nullptr;
-    RT_HIP(hipEventCreate(&e));
-    sc.ev.push_back(e);
-  }
-  const size_t cur = c->grid_cur;
-  hipError_t e = hipSuccess;
-  for (int pass = 0; pass < kPasses && e == hipSuccess; ++pass)
-    for (size_t j = 0; j < n && e == hipSuccess; ++j) {
-      select_grid(c, j);
-      grid_kparams(c, kp);
-      const size_t lds = rtk::grid_lds_bytes(c->grid_placement, kp.grid_n_items, kp.grid_n_cells);
-      const size_t k = 2 * (pass * n + j);
-      e = hipEventRecord(sc.ev[k], c->stream);
-      if (e == hipSuccess) e = rtk::launch_render(v, blocks, lds, c->stream, kp);
-      if (e == hipSuccess) e = hipEventRecord(sc.ev[k + 1], c->stream);
-    }
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  // the fastest candidate (best of the passes), kept only if it beats the
-  // builder's grid by kGridTuneGain: within that the pick would follow
-  // timing noise from run to run
-  constexpr float kGridTuneGain = 0.99f;
-  std::vector<float> t(n, INFINITY);
-  for (size_t j = 0; j < n && e == hipSuccess; ++j)
-    for (int pass = 0; pass < kPasses && e == hipSuccess; ++pass) {
-      float ms = 0.0f;
-      const size_t k = 2 * (pass * n + j);
-      e = hipEventElapsedTime(&ms, sc.ev[k], sc.ev[k + 1]);
-      t[j] = std::min(t[j], ms);
-    }
-  size_t best = 0;
-  for (size_t j = 1; j < n; ++j)
-    if (t[j] < t[best]) best = j;
-  if (!(t[best] < kGridTuneGain * t[0])) best = 0;
-  select_grid(c, e == hipSuccess ? best : cur);
-  if (e != hipSuccess) return hip_fail(e);
-  c->tune_ms.assign(t.begin(), t.end());
-  c->order_key.clear();  // the next pilot schedules for the grid kept
-  if (scale_out) *scale_out = c->grid_scale;
-  return RT_OK;
-}
-
-int rt_internal_grid_candidates(rt_context *c, double *scales, float *ms, size_t n_out, size_t *n) {
-  if (!c || !n || (n_out && (!scales || !ms))) return RT_ERR_INVALID;
-  *n = c->grid_alts.size();
-  for (size_t j = 0; j < n_out && j < c->grid_alts.size(); ++j) {
-    scales[j] = c->grid_alts[j].scale;
-    ms[j] = j < c->tune_ms.size() ? c->tune_ms[j] : NAN;
-  }
-  return RT_OK;
-}
-
 // Host-only view of what rt_scene_upload would build (no device needed):
 // tests/test_host.py checks the builder's invariants on CPU, and
 // tools/host_sanitize.sh runs it under ASan / UBSan.  See include/rt.h for
@@ -998,24 +826,6 @@ int rt_internal_accel_info(const rt_scene_view *s, int grid_placement, double gr
   static const uint64_t kPlaceOut[3] = {RT_GRID_GLOBAL, RT_GRID_LDS, RT_GRID_CELLS_LDS};
   v[16] = cells ? kPlaceOut[a.grid_placement] : 0u;
   v[17] = (uint64_t)std::llround(a.grid_scale * 1000.0);
-  // the candidate grids of rt_tune_grid and their invariants (as 11 / 12, and
-  // each fits the placement's LDS budget)
-  bool alts_ok = true;
-  const size_t lds_max = o.wide ? rtk::kGridLdsMaxWide : rtk::kGridLdsMax;
-  for (const rtk::grid_geom &q : a.grid_alts) {
-    const uint64_t qi = q.items.size() / 4, qc = q.cells.size();
-    alts_ok = alts_ok && qc == (uint64_t)q.nx * q.nz && qc > 0 &&
-              rtk::grid_lds_bytes(a.grid_placement, (long long)qi, (long long)qc) <= lds_max;
-    for (uint64_t i = 0; i < qc && alts_ok; ++i) {
-      const uint32_t first = q.cells[i] >> 4, cnt = q.cells[i] & 15u;
-      const uint64_t next = i + 1 < qc ? (q.cells[i + 1] >> 4) : qi;
-      const int x = (int)(i % q.nx), z = (int)(i / q.nx);
-      const bool ring = x == 0 || z == 0 || x == q.nx - 1 || z == q.nz - 1;
-      alts_ok = first + cnt == next && !(ring && cnt);
-    }
-  }
-  v[18] = a.grid_alts.size();
-  v[19] = alts_ok ? 1u : 0u;
   std::memcpy(out, v, std::min<size_t>(n_out, RT_ACCEL_INFO_N) * sizeof(uint64_t));
   return RT_OK;
 }

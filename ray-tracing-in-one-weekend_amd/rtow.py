@@ -37,7 +37,7 @@ RT_FLAG_LAYER_BVH = 1 << 12  # layer scenes: walk the layer BVH instead of the l
 RT_CHUNK_SPP = 64  # include/rt.h: kept for compatibility (pixel sums are exact integers, units split evenly)
 RT_TONEMAP_CPU, RT_TONEMAP_GPU = 0, 1  # write_color of src/cpu (fp64) / src/gpu (fp32)
 RT_KAT_SPHERE_HIT, RT_KAT_REFLECT, RT_KAT_REFRACT, RT_KAT_REFLECTANCE = 0, 1, 2, 3
-ABI_VERSION = 4
+ABI_VERSION = 5
 # rt_context_set_option (include/rt.h): placement / shape / launch options, never semantics
 RT_OPT_GRID_PLACEMENT, RT_OPT_GRID_SCALE, RT_OPT_BVH_LEAF = 1, 2, 3
 RT_OPT_BVH_COLLAPSE, RT_OPT_BVH_SIDE, RT_OPT_LAUNCH_SAMPLES = 4, 5, 6
@@ -127,10 +127,6 @@ def lib():
         L.rt_render.argtypes = [ctypes.c_void_p, ctypes.POINTER(Camera), ctypes.POINTER(Params),
                                 ctypes.c_void_p, ctypes.POINTER(Stats)]
         L.rt_collect_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(Stats)]
-        if hasattr(L, "rt_tune_grid"):
-            L.rt_tune_grid.argtypes = [ctypes.c_void_p, ctypes.POINTER(Camera), ctypes.POINTER(Params), d3]
-            L.rt_internal_grid_candidates.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                                      ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
         L.rt_reset_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         if hasattr(L, "rt_render_progress"):
             L.rt_render_progress.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32),
@@ -361,26 +357,6 @@ class Context:
                                     ctypes.c_void_p(dev_ptr), ctypes.c_void_p(stream)),
               "rt_render_async")
 
-    def tune_grid(self, cam, params):
-        """rt_tune_grid: time a short pilot of this frame geometry with each
-        candidate layer-grid cell size of the uploaded scene, keep the fastest
-        (the image is the same for every one); returns its cell scale (0.0
-        without a grid)."""
-        g = ctypes.c_double()
-        check(lib().rt_tune_grid(self._h, ctypes.byref(cam), ctypes.byref(params), ctypes.byref(g)),
-              "rt_tune_grid")
-        return g.value
-
-    def grid_candidates(self):
-        """rt_internal_grid_candidates: [(cell scale, last tune pilot ms or nan)]."""
-        n = ctypes.c_size_t()
-        check(lib().rt_internal_grid_candidates(self._h, None, None, 0, ctypes.byref(n)),
-              "rt_internal_grid_candidates")
-        sc, ms = np.zeros(max(1, n.value), np.float64), np.zeros(max(1, n.value), np.float32)
-        check(lib().rt_internal_grid_candidates(self._h, sc.ctypes.data, ms.ctypes.data, n.value,
-                                                ctypes.byref(n)), "rt_internal_grid_candidates")
-        return [(float(a), float(b)) for a, b in zip(sc[:n.value], ms[:n.value])]
-
     def tonemap_async(self, dev_sums, n_pixels, spp, dev_out, mode=RT_TONEMAP_CPU, stream=0):
         """write_color on the device: fp32 sums -> bytes, both device pointers."""
         check(lib().rt_tonemap_async(self._h, ctypes.c_void_p(dev_sums), n_pixels, spp, mode,
@@ -425,8 +401,7 @@ def device_kat(kind, cases, device=0):
 ACCEL_INFO_KEYS = ("nodes_per_order", "bvh_slots", "layer_mode", "extra_pair0", "n_extra_pairs",
                    "grid_nx", "grid_nz", "grid_items", "grid_lds_bytes", "grid_fits_lds",
                    "max_items_per_cell", "grid_starts_ok", "grid_ring_empty", "oref_milli",
-                   "layer_slots", "listed_cells", "grid_placement", "grid_scale_milli",
-                   "grid_candidates", "grid_candidates_ok")
+                   "layer_slots", "listed_cells", "grid_placement", "grid_scale_milli")
 
 
 def accel_info(scene, grid_mode="auto", grid_scale=0.0):

@@ -50,8 +50,6 @@ def expected(rtow, personality, extra, w, h, spp, depth, seed):
     ("cpu_ray_tracer", ["--camera", "gpu"]),
     ("cpu_ray_tracer", ["--spheres", "50"]),
     ("cpu_ray_tracer", ["--accel", "scan"]),
-    ("cpu_ray_tracer", ["--spheres", "50", "--tune-grid"]),
-    ("gpu_ray_tracer", ["--tune-grid"]),
 ], ids=lambda x: x if isinstance(x, str) else "_".join(a.strip("-") for a in x) or "defaults")
 def test_cli_ppm_equals_oracle(rtow, personality, extra):
     w, h, spp, depth, seed = 64, 36, 5, 50, 11

@@ -36,7 +36,6 @@ def main():
     ap.add_argument("--flags", default="", help="extra '+'-joined RT_FLAG_ names")
     ap.add_argument("--units", type=int, default=0, help="rt_params.units (0: automatic)")
     ap.add_argument("--grid-scale", type=float, default=0.0)
-    ap.add_argument("--grid-tune", action="store_true", help="rt_tune_grid before the renders (opt-in)")
     ap.add_argument("--row-block", type=int, default=8, help="rows per interleaved band")
     a = ap.parse_args()
     import rtow
@@ -54,14 +53,13 @@ def main():
     for r in a.rank:
         p = rtow.make_params(w, h, spp, seed=0, flags=flags, rank=r, world=a.world, units=a.units,
                              row_block=a.row_block)
-        g = ctx.tune_grid(cam, p) if a.grid_tune else 0.0
         for _ in range(a.reps):
             t = time.perf_counter()
             img, st = ctx.render(cam, p)
             wall = time.perf_counter() - t
             rec = {"preset": a.preset, "frame": f"{w}x{h}x{spp}", "spheres": scene.n, "world": a.world,
                    "rank": r, "local_rows": p.local_rows, "row_block": a.row_block, "grid_mode": a.grid_mode, "flags": a.flags,
-                   "units": a.units, "grid_tuned_scale": round(g, 4),
+                   "units": a.units,
                    "kernel_ms": round(st.kernel_ms, 1), "launches": getattr(st, "launches", 1),
                    "wall_ms_incl_copy": round(wall * 1e3, 1), "segments": st.segments,
                    "mray_s": round(st.segments / st.kernel_ms / 1e3, 1), "upload_s": round(t_up, 2)}

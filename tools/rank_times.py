@@ -25,8 +25,6 @@ def main():
     ap.add_argument("--pilot", action="store_true",
                     help="RT_FLAG_PILOT_SCHEDULE; every share is rendered twice and the second "
                          "(with the cached tile order) is timed")
-    ap.add_argument("--grid-tune", action="store_true",
-                    help="rt_tune_grid per share, as bench.py --grid-tune does per rank")
     a = ap.parse_args()
     import rtow
     ctx = rtow.Context(0)
@@ -35,8 +33,6 @@ def main():
     flags = rtow.RT_FLAG_ACCEL_BVH | (rtow.RT_FLAG_PILOT_SCHEDULE if a.pilot else 0)
     reps = 2 if a.pilot else 1
     p = rtow.make_params(a.w, a.h, a.spp, seed=0, flags=flags)
-    if a.grid_tune:
-        ctx.tune_grid(cam, p)
     for _ in range(reps):
         _, st = ctx.render(cam, p)
     full = st.kernel_ms
@@ -47,8 +43,6 @@ def main():
             for r in range(g):
                 p = rtow.make_params(a.w, a.h, a.spp, seed=0, flags=flags, rank=r, world=g,
                                      row_block=a.row_block, units=u)
-                if a.grid_tune:
-                    ctx.tune_grid(cam, p)
                 for _ in range(reps):
                     _, st = ctx.render(cam, p)
                 ms.append(st.kernel_ms)
