@@ -401,6 +401,9 @@ def main():
             "lane_efficiency": round(segments / (64.0 * wave_steps), 4) if wave_steps else None,
             "kernel_ms_avg_rank0": round(k_avg_s * 1e3, 3),
             "accel": a.accel,
+            "grid_cell_scale": round(ctx.grid_scale(), 4) if a.accel == "bvh" else None,
+            "grid_cell_scale_note": "the layer grid's cell scale RT_OPT_GRID_FIT fitted to this frame geometry "
+                                    "(host model, first frame; DESIGN.md 3.3)",
             "walk": {"bvh": "layer grid (per-lane DDA) + extras scanned", "scan": "brute force",
                      "layer_bvh": "wave-uniform layer BVH + extras scanned"}[a.accel],
             "schedule": "launch order" if a.no_pilot else

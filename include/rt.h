@@ -29,8 +29,9 @@
 extern "C" {
 #endif
 
-/* 5: rt_tune_grid and rt_internal_grid_candidates removed, RT_ACCEL_INFO_N 18,
- * t_min in units of the unnormalised direction (round 5) */
+/* 5 (round 5): rt_tune_grid and rt_internal_grid_candidates removed,
+ * RT_ACCEL_INFO_N 18, RT_OPT_GRID_FIT, rt_internal_grid_fit /
+ * rt_internal_grid_scale, t_min in units of the unnormalised direction */
 #define RT_ABI_VERSION 5
 
 typedef enum {
@@ -245,7 +246,14 @@ typedef enum {
    * holds at least one sample per pixel.  At most 65536 launches per render:
    * a smaller budget is raised to total samples / 65536.
    * rt_internal_launch_plan shows the plan. */
-  RT_OPT_LAUNCH_SAMPLES = 6
+  RT_OPT_LAUNCH_SAMPLES = 6,
+  /* 1 (default): the layer grid's cell size is fitted to each frame geometry
+   * (camera and frame size) on its first render, by a host-side model of the
+   * walk's cost over the builder's candidate sizes (scale s0 (1 + 0.01 k),
+   * k = 0..30, that fit the grid's LDS placement); 0: the builder's grid.
+   * No fitting either when RT_OPT_GRID_SCALE is set (non-zero).  Set before
+   * rt_scene_upload.  Scheduling only: every size renders the same image. */
+  RT_OPT_GRID_FIT = 7
 } rt_option;
 enum { RT_GRID_AUTO = 0, RT_GRID_LDS = 1, RT_GRID_CELLS_LDS = 2, RT_GRID_GLOBAL = 3 };
 int rt_context_set_option(rt_context *ctx, int option, double value);
@@ -368,6 +376,19 @@ int rt_internal_accel_info(const rt_scene_view *scene, int grid_placement, doubl
  * For tests. */
 #define RT_LAUNCH_PLAN_N 5
 int rt_internal_launch_plan(const rt_params *params, double launch_samples, uint64_t *out, size_t n_out);
+
+/* Host only (no device): the layer-grid cell scale RT_OPT_GRID_FIT would
+ * pick for `scene` (default builder options, the automatic placement) seen by
+ * `cam` in a width x height frame; *scale = 0 without a grid in an LDS
+ * placement.  With costs != NULL, the modelled cost of each candidate that
+ * fits: (scale, cost) pairs, min(n_costs, *n) of them (*n = their count).
+ * For tests and tools. */
+int rt_internal_grid_fit(const rt_scene_view *scene, const rt_camera *cam, int width, int height, double *scale,
+                         double *costs, size_t n_costs, size_t *n);
+/* The cell scale of the context's current layer grid (after RT_OPT_GRID_FIT
+ * refits it for a render's frame geometry); 0 without a grid.  For tests and
+ * the bench record. */
+int rt_internal_grid_scale(rt_context *ctx, double *scale);
 
 /* Host only (no device): for each sphere of `scene`, 1 if the kernel's
  * opaque-inside rule applies to it (a sealed lambertian sphere: no other

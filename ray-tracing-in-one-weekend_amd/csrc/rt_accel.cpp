@@ -491,7 +491,8 @@ double max_albedo(const rt_scene_view *s) {
 }
 
 
-void build_accel(const rt_scene_view *s, const accel_options &o, accel_build &a) {
+void build_accel(const rt_scene_view *s, const accel_options &o, accel_build &a, grid_fitter **fitter) {
+  if (fitter) *fitter = nullptr;
   const uint32_t n = s->n;
   a = accel_build{};
   a.n = n;
@@ -588,6 +589,152 @@ void build_accel(const rt_scene_view *s, const accel_options &o, accel_build &a)
   a.grid_nz = bb.grid_nz;
   a.grid_scale = bb.grid_scale;
   a.grid_placement = bb.grid_cells.empty() ? kGridGlobal : place;
+  // the builder's layer split and boxes go on into the grid fitter
+  if (fitter && !bb.grid_cells.empty())
+    *fitter = grid_fitter::make_from(s, o, a.grid_placement, bb.grid_scale, &bb);
+}
+
+// ---------------------------------------------------------- grid fitter --
+struct grid_fitter::impl {
+  // the scene's arrays (the view the builder reads points into them)
+  std::vector<float> cx, cy, cz, radius, albedo, param;
+  std::vector<uint32_t> kind;
+  rt_scene_view view{};
+  mutable bvh_builder bb;  // after run(): boxes, layer order; build_grid rebuilds the grid
+  int placement = kGridGlobal;
+  size_t lds_max = 0;
+  double s0 = 1.0;
+  // the grid at scale s into bb's grid fields; false if it does not fit the placement
+  bool grid_at(double scale) const {
+    bb.grid_scale = scale;
+    bb.build_grid(&view, bb.n_layer);
+    if (bb.grid_cells.empty()) return false;
+    const long long items = (long long)(bb.grid_items.size() / 4), cells = (long long)bb.grid_cells.size();
+    if (placement == kGridLds)
+      return items < 4096 && grid_lds_bytes(kGridLds, items, cells) <= lds_max;
+    return items < 65536 && grid_lds_bytes(kGridCells, items, cells) <= lds_max;
+  }
+};
+
+grid_fitter *grid_fitter::make(const rt_scene_view *s, const accel_options &o, int placement, double scale0) {
+  return make_from(s, o, placement, scale0, nullptr);
+}
+
+// builder: a bvh_builder that has run on s (build_accel's, moved here), or null
+grid_fitter *grid_fitter::make_from(const rt_scene_view *s, const accel_options &o, int placement, double scale0,
+                                    void *builder) {
+  if (placement != kGridLds && placement != kGridCells) return nullptr;
+  grid_fitter *f = new grid_fitter();
+  impl *q = f->p_ = new impl();
+  const uint32_t n = s->n;
+  q->cx.assign(s->cx, s->cx + n);
+  q->cy.assign(s->cy, s->cy + n);
+  q->cz.assign(s->cz, s->cz + n);
+  q->radius.assign(s->radius, s->radius + n);
+  q->kind.assign(s->mat_kind, s->mat_kind + n);
+  q->albedo.assign(s->albedo_rgb, s->albedo_rgb + 3 * (size_t)n);
+  q->param.assign(s->mat_param, s->mat_param + n);
+  q->view = *s;
+  q->view.cx = q->cx.data();
+  q->view.cy = q->cy.data();
+  q->view.cz = q->cz.data();
+  q->view.radius = q->radius.data();
+  q->view.mat_kind = q->kind.data();
+  q->view.albedo_rgb = q->albedo.data();
+  q->view.mat_param = q->param.data();
+  if (builder) {
+    q->bb = std::move(*static_cast<bvh_builder *>(builder));
+  } else {
+    q->bb.max_leaf = std::max(1, std::min(bvh_builder::kLeaf, o.bvh_leaf));
+    q->bb.collapse_area = o.collapse;
+    q->bb.side_weight = o.side;
+    q->bb.grid_scale = scale0;
+    q->bb.run(&q->view);
+  }
+  q->placement = placement;
+  q->lds_max = o.wide ? kGridLdsMaxWide : kGridLdsMax;
+  q->s0 = scale0;
+  if (!q->bb.layer_mode || !q->grid_at(scale0)) {
+    delete f;
+    return nullptr;
+  }
+  return f;
+}
+
+grid_fitter::~grid_fitter() { delete p_; }
+double grid_fitter::scale0() const { return p_->s0; }
+
+double grid_fitter::choose(const rt_camera &cam, int width, int height,
+                           std::vector<std::pair<double, double>> *costs) const {
+  const impl &q = *p_;
+  if (costs) costs->clear();
+  double best = q.s0, best_cost = INFINITY;
+  for (int k = 0; k <= kFitSteps; ++k) {
+    const double scale = q.s0 * (1.0 + 0.01 * k);
+    if (!q.grid_at(scale)) continue;
+    const bvh_builder &b = q.bb;
+    const int nx = b.grid_nx, nz = b.grid_nz;
+    const double g = b.grid_g;
+    // where 64 x 64 camera directions over the frame meet the layer plane
+    std::vector<double> w((size_t)nx * nz, 0.0);
+    constexpr int kS = 64;
+    for (int j = 0; j < kS; ++j)
+      for (int i = 0; i < kS; ++i) {
+        double fs = (i + 0.5) / kS, ft = (j + 0.5) / kS;
+        if (cam.model == RT_CAMERA_GPU) {
+          fs = fs * width - 0.5;
+          ft = ft * height - 0.5;
+        }
+        double d[3];
+        for (int a = 0; a < 3; ++a) d[a] = cam.corner[a] + fs * cam.horiz[a] + ft * cam.vert[a] - cam.eye[a];
+        if (!(d[1] != 0.0)) continue;
+        const double t = (b.layer_cy - cam.eye[1]) / d[1];
+        if (!(t > 0.0)) continue;
+        const double x = (cam.eye[0] + t * d[0] - b.grid_x0) / g, z = (cam.eye[2] + t * d[2] - b.grid_z0) / g;
+        if (!(x >= 0.0 && x < nx && z >= 0.0 && z < nz)) continue;
+        w[(size_t)z * nx + (size_t)x] += 1.0;
+      }
+    // 3 x 3 box-smoothed weight of each cell times its item count
+    double sw = 0.0, swi = 0.0;
+    for (int z = 0; z < nz; ++z)
+      for (int x = 0; x < nx; ++x) {
+        double v = 0.0;
+        for (int dz = -1; dz <= 1; ++dz)
+          for (int dx = -1; dx <= 1; ++dx) {
+            const int zz = z + dz, xx = x + dx;
+            if (zz >= 0 && zz < nz && xx >= 0 && xx < nx) v += w[(size_t)zz * nx + xx];
+          }
+        sw += v;
+        swi += v * (double)(b.grid_cells[(size_t)z * nx + x] & 15u);
+      }
+    if (!(sw > 0.0)) return q.s0;  // the camera does not see the layer: the builder's grid
+    const double cost = (swi / sw + kFitCellCost) / g;
+    if (costs) costs->push_back({scale, cost});
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = scale;
+    }
+  }
+  return best;
+}
+
+bool grid_fitter::build(double scale, grid_geom &out) const {
+  const impl &q = *p_;
+  if (!q.grid_at(scale)) return false;
+  const bvh_builder &b = q.bb;
+  out.cells = b.grid_cells;
+  out.items = b.grid_items;
+  out.x0 = b.grid_x0;
+  out.z0 = b.grid_z0;
+  out.xi = b.grid_xi;
+  out.zi = b.grid_zi;
+  out.x1 = b.grid_x1;
+  out.z1 = b.grid_z1;
+  out.g = b.grid_g;
+  out.nx = b.grid_nx;
+  out.nz = b.grid_nz;
+  out.scale = b.grid_scale;
+  return true;
 }
 
 }  // namespace rtk

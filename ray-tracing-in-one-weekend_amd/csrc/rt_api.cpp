@@ -47,6 +47,17 @@ struct rt_context {
   float grid_x0 = 0, grid_z0 = 0, grid_xi = 0, grid_zi = 0, grid_x1 = 0, grid_z1 = 0, grid_g = 0;
   int grid_nx = 0, grid_nz = 0;
   double grid_scale = 1.0;
+  // the layer grid's cell size fitted per frame geometry (rtk::grid_fitter,
+  // DESIGN.md 3.3): the fitter, the geometry its grid was fitted for, and the
+  // host copy the last refit uploads from (ev_fit: after that copy)
+  rtk::grid_fitter *fitter = nullptr;
+  std::vector<uint64_t> fit_key;
+  rtk::grid_geom fit_grid;
+  size_t cells_cap = 0, items_cap = 0;  // d_grid_cells / d_grid_items capacity (u32 / items)
+  hipEvent_t ev_fit = nullptr;
+  bool fit_pending = false;
+  bool grid_fit = true;         // RT_OPT_GRID_FIT
+  bool grid_scale_set = false;  // RT_OPT_GRID_SCALE given: no fitting
   unsigned long long *d_counters = nullptr;
   float *d_frame = nullptr;
   size_t frame_floats = 0;
@@ -132,6 +143,10 @@ void free_scene(rt_context *c) {
   (void)hipFree(c->d_shade);
   (void)hipFree(c->d_grid_cells);
   (void)hipFree(c->d_grid_items);
+  delete c->fitter;
+  c->fitter = nullptr;
+  c->fit_key.clear();
+  c->cells_cap = c->items_cap = 0;
   c->d_grid_cells = nullptr;
   c->d_grid_items = nullptr;
   c->grid_nx = c->grid_nz = 0;
@@ -256,6 +271,7 @@ void rt_context_destroy(rt_context *c) {
   (void)hipFree(c->d_thr32);
   for (hipEvent_t ev : c->ev_launch) (void)hipEventDestroy(ev);
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);
+  if (c->ev_fit) (void)hipEventDestroy(c->ev_fit);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -275,6 +291,11 @@ int rt_context_set_option(rt_context *c, int option, double v) {
     case RT_OPT_GRID_SCALE:
       if (!dflt && !(v >= 0.05 && v <= 20.0)) return RT_ERR_INVALID;
       c->opt.grid_scale = dflt ? 1.0 : v;
+      c->grid_scale_set = !dflt;
+      return RT_OK;
+    case RT_OPT_GRID_FIT:
+      if (v != 0.0 && v != 1.0) return RT_ERR_INVALID;
+      c->grid_fit = v != 0.0;
       return RT_OK;
     case RT_OPT_BVH_LEAF:
       if (v != std::floor(v) || v < 0 || v > 4) return RT_ERR_INVALID;
@@ -302,12 +323,20 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
   rtk::accel_build a;
   rtk::accel_options o = c->opt;
   o.wide = rtk::max_albedo(s) > 1.0;
-  rtk::build_accel(s, o, a);
+  rtk::grid_fitter *fitter = nullptr;
+  rtk::build_accel(s, o, a, c->grid_fit && !c->grid_scale_set ? &fitter : nullptr);
 
   RT_HIP(hipSetDevice(c->device));
   // renders enqueued on caller streams may still read the old scene
-  RT_HIP(hipDeviceSynchronize());
+  {
+    const hipError_t e0 = hipDeviceSynchronize();
+    if (e0 != hipSuccess) {
+      delete fitter;
+      return hip_fail(e0);
+    }
+  }
   free_scene(c);
+  c->fitter = fitter;
   hipError_t e = upload_vec(&c->d_geom, a.scan_geom, c->stream);
   if (e == hipSuccess) e = upload_vec(&c->d_bvh_geom, a.bvh_geom, c->stream);
   if (e == hipSuccess) e = upload_vec(&c->d_nodes, a.nodes, c->stream);
@@ -316,6 +345,8 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
   if (e == hipSuccess && !a.grid_cells.empty()) {
     e = upload_vec(&c->d_grid_cells, a.grid_cells, c->stream);
     if (e == hipSuccess) e = upload_vec(&c->d_grid_items, a.grid_items, c->stream);
+    c->cells_cap = a.grid_cells.size();
+    c->items_cap = a.grid_items.size() / 4;
     c->grid_n_items = a.grid_items.size() / 4;
     c->grid_placement = a.grid_placement;
   }
@@ -543,6 +574,56 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
   const long long tiles = (long long)kp.tiles_x * tiles_y;
   const unsigned blocks = (unsigned)((tiles + rtk::kWavesPerBlock - 1) / rtk::kWavesPerBlock);
   const bool grid = c->d_grid_cells && !(prm->flags & RT_FLAG_LAYER_BVH);
+  if (grid && c->fitter && (prm->flags & RT_FLAG_ACCEL_BVH)) {
+    // the layer grid's cell size for this frame geometry (rtk::grid_fitter:
+    // a host-side model, once per geometry; the image is the same for every
+    // size).  The new grid is copied into the context's buffers on st, after
+    // every earlier render (renders of one context are serialised).
+    std::vector<uint64_t> key = {(uint64_t)prm->width, (uint64_t)prm->height};
+    const uint32_t *cw = reinterpret_cast<const uint32_t *>(cam);
+    for (size_t k = 0; k < sizeof(rt_camera) / 4; ++k) key.push_back(cw[k]);
+    if (key != c->fit_key) {
+      const double scale = c->fitter->choose(*cam, prm->width, prm->height, nullptr);
+      if (scale != c->grid_scale) {
+        if (c->fit_pending) RT_HIP(hipEventSynchronize(c->ev_fit));  // fit_grid is still being read
+        c->fit_pending = false;
+        rtk::grid_geom &q = c->fit_grid;
+        if (!c->fitter->build(scale, q)) return RT_ERR_INVALID;  // (every candidate fits: unreachable)
+        if (q.cells.size() > c->cells_cap || q.items.size() / 4 > c->items_cap) {
+          RT_HIP(hipStreamSynchronize(st));
+          (void)hipFree(c->d_grid_cells);
+          (void)hipFree(c->d_grid_items);
+          c->d_grid_cells = nullptr;
+          c->d_grid_items = nullptr;
+          c->cells_cap = c->items_cap = 0;
+          RT_HIP(hipMalloc(&c->d_grid_cells, q.cells.size() * sizeof(uint32_t)));
+          RT_HIP(hipMalloc(&c->d_grid_items, q.items.size() * sizeof(float)));
+          c->cells_cap = q.cells.size();
+          c->items_cap = q.items.size() / 4;
+        }
+        RT_HIP(hipMemcpyAsync(c->d_grid_cells, q.cells.data(), q.cells.size() * sizeof(uint32_t),
+                              hipMemcpyHostToDevice, st));
+        RT_HIP(hipMemcpyAsync(c->d_grid_items, q.items.data(), q.items.size() * sizeof(float), hipMemcpyHostToDevice,
+                              st));
+        if (!c->ev_fit) RT_HIP(hipEventCreateWithFlags(&c->ev_fit, hipEventDisableTiming));
+        RT_HIP(hipEventRecord(c->ev_fit, st));
+        c->fit_pending = true;
+        c->grid_n_items = q.items.size() / 4;
+        c->grid_x0 = q.x0;
+        c->grid_z0 = q.z0;
+        c->grid_xi = q.xi;
+        c->grid_zi = q.zi;
+        c->grid_x1 = q.x1;
+        c->grid_z1 = q.z1;
+        c->grid_g = q.g;
+        c->grid_nx = q.nx;
+        c->grid_nz = q.nz;
+        c->grid_scale = q.scale;
+        grid_kparams(c, kp);
+      }
+      c->fit_key = key;
+    }
+  }
   const int place = grid ? c->grid_placement : rtk::kGridGlobal;
   const sum_fmt fmt = sum_format(prm->spp, prm->max_depth, c->max_albedo);
   const int v = render_variant(c, prm, fmt.wide);
@@ -827,6 +908,34 @@ int rt_internal_accel_info(const rt_scene_view *s, int grid_placement, double gr
   v[16] = cells ? kPlaceOut[a.grid_placement] : 0u;
   v[17] = (uint64_t)std::llround(a.grid_scale * 1000.0);
   std::memcpy(out, v, std::min<size_t>(n_out, RT_ACCEL_INFO_N) * sizeof(uint64_t));
+  return RT_OK;
+}
+
+int rt_internal_grid_fit(const rt_scene_view *s, const rt_camera *cam, int width, int height, double *scale,
+                         double *costs, size_t n_costs, size_t *n) {
+  if (!rtk::scene_ok(s) || !cam || !scale || width < 1 || height < 1 || (n_costs && !costs)) return RT_ERR_INVALID;
+  rtk::accel_options o;
+  o.wide = rtk::max_albedo(s) > 1.0;
+  rtk::accel_build a;
+  rtk::grid_fitter *f = nullptr;
+  rtk::build_accel(s, o, a, &f);
+  *scale = 0.0;
+  if (n) *n = 0;
+  if (!f) return RT_OK;
+  std::vector<std::pair<double, double>> cs;
+  *scale = f->choose(*cam, width, height, &cs);
+  delete f;
+  if (n) *n = cs.size();
+  for (size_t i = 0; i < cs.size() && i < n_costs; ++i) {
+    costs[2 * i] = cs[i].first;
+    costs[2 * i + 1] = cs[i].second;
+  }
+  return RT_OK;
+}
+
+int rt_internal_grid_scale(rt_context *c, double *scale) {
+  if (!c || !scale) return RT_ERR_INVALID;
+  *scale = c->d_grid_cells ? c->grid_scale : 0.0;
   return RT_OK;
 }
 

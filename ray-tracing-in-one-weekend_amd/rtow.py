@@ -40,7 +40,7 @@ RT_KAT_SPHERE_HIT, RT_KAT_REFLECT, RT_KAT_REFRACT, RT_KAT_REFLECTANCE = 0, 1, 2,
 ABI_VERSION = 5
 # rt_context_set_option (include/rt.h): placement / shape / launch options, never semantics
 RT_OPT_GRID_PLACEMENT, RT_OPT_GRID_SCALE, RT_OPT_BVH_LEAF = 1, 2, 3
-RT_OPT_BVH_COLLAPSE, RT_OPT_BVH_SIDE, RT_OPT_LAUNCH_SAMPLES = 4, 5, 6
+RT_OPT_BVH_COLLAPSE, RT_OPT_BVH_SIDE, RT_OPT_LAUNCH_SAMPLES, RT_OPT_GRID_FIT = 4, 5, 6, 7
 RT_GRID_AUTO, RT_GRID_LDS, RT_GRID_CELLS_LDS, RT_GRID_GLOBAL = 0, 1, 2, 3
 GRID_PLACEMENTS = {"auto": RT_GRID_AUTO, "lds": RT_GRID_LDS, "cells": RT_GRID_CELLS_LDS, "global": RT_GRID_GLOBAL}
 
@@ -343,6 +343,14 @@ class Context:
         check(lib().rt_scene_upload(self._h, ctypes.byref(v)), "rt_scene_upload")
         self.scene = scene
 
+    def grid_scale(self):
+        """The cell scale of the context's current layer grid (RT_OPT_GRID_FIT
+        refits it per frame geometry); 0.0 without a grid."""
+        lib().rt_internal_grid_scale.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)]
+        g = ctypes.c_double()
+        check(lib().rt_internal_grid_scale(self._h, ctypes.byref(g)), "rt_internal_grid_scale")
+        return g.value
+
     def render(self, cam, params):
         """Render synchronously; returns (sums float32 [rows, W, 3], Stats)."""
         out = np.zeros((params.local_rows, params.width, 3), np.float32)
@@ -413,6 +421,22 @@ def accel_info(scene, grid_mode="auto", grid_scale=0.0):
     check(lib().rt_internal_accel_info(ctypes.byref(v), GRID_PLACEMENTS[grid_mode], float(grid_scale),
                                        out.ctypes.data, out.size), "rt_internal_accel_info")
     return {k: int(x) for k, x in zip(ACCEL_INFO_KEYS, out)}
+
+
+def grid_fit(scene, cam, width, height):
+    """What RT_OPT_GRID_FIT picks for `scene` seen by `cam` in a width x height
+    frame, computed on the host (rt_internal_grid_fit; no device): (cell scale
+    or 0.0 without an LDS grid, [(candidate scale, modelled cost)])."""
+    L = lib()
+    L.rt_internal_grid_fit.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_double), ctypes.c_void_p, ctypes.c_size_t,
+                                       ctypes.POINTER(ctypes.c_size_t)]
+    v = scene.view()
+    sc, n = ctypes.c_double(), ctypes.c_size_t()
+    costs = np.zeros(2 * 64, np.float64)
+    check(L.rt_internal_grid_fit(ctypes.byref(v), ctypes.byref(cam), width, height, ctypes.byref(sc),
+                                 costs.ctypes.data, 64, ctypes.byref(n)), "rt_internal_grid_fit")
+    return sc.value, [(float(costs[2 * i]), float(costs[2 * i + 1])) for i in range(min(64, n.value))]
 
 
 def sealed(scene):

@@ -203,7 +203,7 @@ def test_ppm_writer_p3_and_p6(rtow, tmp_path):
 def test_abi_exports_every_declared_symbol(rtow):
     hdr = open(os.path.join(ROOT, "include", "rt.h")).read()
     names = sorted(set(re.findall(r"^\s*(?:[\w\*\s]+?)\b(rt_\w+)\s*\(", hdr, re.M)))
-    assert len(names) == 25, names
+    assert len(names) == 27, names
     L = rtow.lib()
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
@@ -320,6 +320,29 @@ def test_accel_builder_invariants_on_host(rtow):
     assert big["grid_starts_ok"] == 1 and big["grid_ring_empty"] == 1
     five = rtow.accel_info(rtow.five_scene())
     assert five["layer_mode"] == 0 and five["grid_items"] == 0
+
+
+def test_grid_fit_picks_a_candidate_per_camera(rtow):
+    """RT_OPT_GRID_FIT (rtk::grid_fitter, DESIGN.md 3.3): the host model of
+    the layer walk's cost picks one of the builder's candidate cell scales
+    s0 (1 + 0.01 k) for a camera; deterministic; the builder's scale when the
+    camera does not see the layer; no fitting without an LDS grid.  The picks
+    for the headline frame and C4's frame are the ones the GPU sweeps were
+    checked against (tools/grid_fit_check.py, profiles/r05g_*)."""
+    fin, c4 = rtow.final_scene(), rtow.final_scene(half_extent=50)
+    cam = rtow.camera_cpu(aspect=16 / 9)
+    sc, costs = rtow.grid_fit(fin, cam, 3840, 2160)
+    s0 = rtow.accel_info(fin)["grid_scale_milli"] / 1000.0
+    assert len(costs) >= 20 and abs(costs[0][0] - s0) < 1e-9
+    assert sc == min(costs, key=lambda x: x[1])[0]
+    assert rtow.grid_fit(fin, cam, 3840, 2160) == (sc, costs)
+    assert abs(sc - 1.11) < 1e-9  # the fine sweep's best region (1.11 / 1.00 / 1.22)
+    sc4, costs4 = rtow.grid_fit(c4, rtow.camera_cpu(aspect=1.0), 16384, 16384)
+    s04 = rtow.accel_info(c4)["grid_scale_milli"] / 1000.0
+    assert abs(sc4 / s04 - 1.05) < 1e-3  # (s0 from accel_info is rounded to 1e-3)
+    up = rtow.camera_cpu(lookfrom=(0, 1, 0), lookat=(0, 5, 0.01), aspect=1.0)  # sky only
+    assert rtow.grid_fit(fin, up, 64, 64)[0] == s0
+    assert rtow.grid_fit(rtow.five_scene(), cam, 64, 36)[0] == 0.0
 
 
 def test_accel_builder_on_degenerate_scenes(rtow):
