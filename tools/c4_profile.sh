@@ -27,10 +27,12 @@ for case in $cases; do
   timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_VALU --output-format csv -d $out/${case}_wait -o wait -- python3 $R $A > $out/${case}_wait.log 2>&1
   timeout -s KILL 300 rocprofv3 --pmc TCP_TOTAL_READ_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCC_READ_REQ_LATENCY_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d $out/${case}_tcp -o tcp -- python3 $R $A > $out/${case}_tcp.log 2>&1
   timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $out/${case}_fetch -o fetch -- python3 $R $A > $out/${case}_fetch.log 2>&1
+  timeout -s KILL 300 rocprofv3 --pmc SQC_ICACHE_REQ SQC_ICACHE_MISSES SQC_DCACHE_REQ SQC_DCACHE_MISSES --output-format csv -d $out/${case}_sqc -o sqc -- python3 $R $A > $out/${case}_sqc.log 2>&1
+  timeout -s KILL 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_INSTS_LDS --output-format csv -d $out/${case}_lds -o lds -- python3 $R $A > $out/${case}_lds.log 2>&1
 done
 cd $GRAFT_REPO_ROOT
 for case in $cases; do
-  python3 tools/pmc_traffic.py $out/${case}_sq $out/${case}_wait $out/${case}_tcp $out/${case}_fetch \
+  python3 tools/pmc_traffic.py $out/${case}_sq $out/${case}_wait $out/${case}_tcp $out/${case}_fetch $out/${case}_sqc $out/${case}_lds \
     --kernel "${KERNEL:-render_kernel<false, false, true, false, true}" --workload "$case share spp=$spp" \
     --out $out/${case}_summary.json > /dev/null
 done
