@@ -68,28 +68,48 @@ def test_reference_mode_byte_identical_random_scenes(rtow, case):
     assert segs == gold["segments"]
 
 
-@pytest.mark.slow
 def test_kernel_algorithm_matches_reference_random_scenes(rtow):
-    """The fp32 kernel algorithm against the reference (through the fp64
-    restatement, which the test above pins byte for byte) on the 24 random
-    scenes at 96x54x64: image-mean bias within 0.5 level per channel (half
-    north_star's 1/255) and segments within 1 %.  This is the test that found
-    rt_scene_upload passing metal fuzz above 1 unclamped (the reference's
-    constructors clamp it, material.h:38): biases of up to -1.4 levels and
-    -4 % segments before the fix, at most 0.21 level and -0.7 % after."""
+    """The fp32 kernel algorithm against the reference on the 24 random scenes
+    at 96x54x64 (tests/random_scenes.py: overlapping and nested spheres,
+    negative-radius glass shells, metal fuzz above 1, indices of refraction
+    below 1, spheres sunk into the ground), against the reference's own noise:
+    its image means from 6 independent streams (tests/golden/
+    make_random_noise_golden.py runs oracle/_ref/ref_harness, the reference's
+    src/cpu) and 8 seeds of the kernel algorithm.  Every channel's bias is
+    within 0.1 level (a tenth of north_star's 1/255) and within 5 sigma of
+    the two noises; segments within 1 %.  Measured (round 5):
+    worst bias 0.064 level; 69 of 72 channels within 2.5 sigma, the other
+    three (3.0-4.1 sigma, 0.04-0.06 level) in the two scenes with spheres
+    sunk into the r = 1000 ground.  Round 4's single-render comparison put
+    scene 12 at 0.21 level: the reference's own render-to-render noise there
+    is 0.097 level.  This test also found round 3's unclamped metal fuzz
+    above 1 (material.h:38): biases of up to -1.4 levels before the fix."""
+    import json
     import random_scenes
+    with open(os.path.join(os.path.dirname(__file__), "golden", "ref_random_scenes_means.json")) as f:
+        gold = json.load(f)
     w, spp = 96, 64
     cam = rtow.camera_cpu(aspect=16.0 / 9.0)
-    worst = 0.0
+    worst = worst_z = 0.0
     for case in range(24):
+        g = gold[str(case)]
+        assert (g["width"], g["spp"], g["depth"]) == (w, spp, 50)
+        ref = np.array(g["means"], np.float64)
         scene = random_scenes.free_scene(rtow, case)
-        ref, rseg = reference_render_view(scene, w, 16.0 / 9.0, spp, 50)
-        sums, seg = kernel_render(scene, cam, rtow.make_params(w, ref.shape[0], spp, seed=1))
-        img = rtow.tonemap(sums, spp)
-        bias = img.reshape(-1, 3).astype(np.float64).mean(0) - ref.reshape(-1, 3).astype(np.float64).mean(0)
+        img, segs = [], []
+        for seed in range(1, 9):
+            sums, seg = kernel_render(scene, cam, rtow.make_params(w, int(w * 9 / 16), spp, seed=seed))
+            img.append(rtow.tonemap(sums, spp).reshape(-1, 3).astype(np.float64).mean(0))
+            segs.append(seg)
+        img = np.array(img)
+        bias = img.mean(0) - ref.mean(0)
+        sigma = np.sqrt(img.var(0, ddof=1) / len(img) + ref.var(0, ddof=1) / len(ref))
         worst = max(worst, float(np.abs(bias).max()))
-        assert np.abs(bias).max() <= 0.5, (case, bias)
-        assert abs(seg / rseg - 1.0) <= 0.01, (case, seg, rseg)
+        worst_z = max(worst_z, float(np.abs(bias / sigma).max()))
+        assert np.abs(bias).max() <= 0.1, (case, bias)
+        assert np.abs(bias / sigma).max() <= 5.0, (case, bias, sigma)
+        assert abs(np.mean(segs) / np.mean(g["segments"]) - 1.0) <= 0.01, (case, segs, g["segments"])
+    print("worst bias %.4f level, worst %.2f sigma" % (worst, worst_z))
     assert worst > 0.0
 
 

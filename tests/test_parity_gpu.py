@@ -526,15 +526,18 @@ def test_dense_layer_grid_build_paths(rtow, gpu_ctx, n_small):
         assert np.array_equal(a, b), (n_small, acc)
 
 
-@pytest.mark.parametrize("case", ["one_launch", "units3", "launches", "dither", "global", "depth1"])
+@pytest.mark.parametrize("case", ["one_launch", "units3", "launches", "spp4100", "dither", "global", "depth1"])
 def test_wide_sums_bit_exact_vs_oracle(rtow, gpu_ctx, case, accel):
     """Albedos above 1: the final scene with one lambertian
     sphere at albedo (1.2, 1.5, 0.9) and a metal one at 1.3 renders with
     64-bit pixel sums and the radiance clamp -- bit-exact
     vs the oracle in every walk, through float stores (one launch), 64-bit
     atomics into the context's scratch frame (units 3, or several bounded
-    launches), the dither (4100 spp), the grid in global memory (the default
-    placement is cells in LDS: 3 KB more static LDS), and depth 1 (vcap 1)."""
+    launches), 4100 spp (F = 31 with these albedos: no dither), the dither of
+    the 64-bit format itself (a 2x2 frame at 2^19 spp with the metal sphere
+    at albedo 1.5: vcap = 2^24, F = 62 - 19 - 24 = 19 < 20), the
+    grid in global memory (the default placement is cells in LDS: 3 KB more
+    static LDS), and depth 1 (vcap 1)."""
     import dataclasses
     base = rtow.final_scene()
     alb = base.albedo.copy()
@@ -543,11 +546,17 @@ def test_wide_sums_bit_exact_vs_oracle(rtow, gpu_ctx, case, accel):
     alb[lam] = (1.2, 1.5, 0.9)
     alb[met] = (1.3, 1.3, 1.3)
     alb[0] = (1.02, 1.02, 1.02)  # the ground
+    if case == "dither":
+        alb[met] = (1.5, 1.5, 1.5)
     hot = dataclasses.replace(base, albedo=alb)
     cam = rtow.camera_cpu(aspect=2.0)
-    spp = {"dither": 4100, "units3": 12}.get(case, 24)
-    p = rtow.make_params(48, 24, spp, seed=31, max_depth=1 if case == "depth1" else 50,
+    spp = {"spp4100": 4100, "units3": 12, "dither": 1 << 19}.get(case, 24)
+    w, h = (2, 2) if case == "dither" else (48, 24)
+    p = rtow.make_params(w, h, spp, seed=31, max_depth=1 if case == "depth1" else 50,
                          units=3 if case == "units3" else 0)
+    if case == "dither":  # the 64-bit format's F (rt_api.cpp sum_format) is below 20
+        vcap = min(1.5 ** 49, 2.0 ** 24)
+        assert 62 - int(np.floor(np.log2(spp))) - int(np.ceil(np.log2(vcap))) == 19
     if case == "launches":
         gpu_ctx.set_option(rtow.RT_OPT_LAUNCH_SAMPLES, 48 * 24 * 5)
     try:
