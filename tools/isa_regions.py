@@ -1,0 +1,182 @@
+#!/usr/bin/env python3
+"""Static VALU / SALU instruction counts of the headline render kernel per
+source region (the per-wave-step budget re-derived on the
+current ISA; not part of the product).
+
+Compiles csrc/rt_kernel.hip for gfx950 with the product's flags plus
+-gline-tables-only (line tables only: the code is the same, the totals are
+checked against tools/isa_blocks.py), then attributes every instruction of
+render_kernel<false,false,true,false,true,1,false> to the innermost frame of
+its `.loc` inlined-at chain that lies in a region of REGIONS below (functions
+of rt_kernel.hip or line ranges of the kernel body), helpers (dot3, fma2,
+sqrt_k, ...) counting for their caller's region.  Prints one row per region:
+static VALU, SALU, LDS, memory instructions and whether the region sits in the
+grid's DDA / item loops.
+
+    python tools/isa_regions.py [--s existing.s] [--json out.json]
+"""
+import argparse
+import collections
+import json
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "ray-tracing-in-one-weekend_amd")
+SRC = os.path.join(PKG, "csrc", "rt_kernel.hip")
+KEY = "render_kernelILb0ELb0ELb1ELb0ELb1ELi1ELb0E"
+
+
+def fn_ranges(lines):
+    """(name, first, last) of every top-level function definition (1-based)."""
+    starts = []
+    for i, l in enumerate(lines):
+        m = re.match(r"^(?:__device__|__global__)[^(]*?(\w+)\s*\(", re.sub(r"__launch_bounds__\([^)]*\)", "", l))
+        if m:
+            starts.append((m.group(1), i + 1))
+    out = []
+    for k, (n, s) in enumerate(starts):
+        e = starts[k + 1][1] - 1 if k + 1 < len(starts) else len(lines)
+        out.append((n, s, e))
+    return out
+
+
+def find_line(lines, pat, after=0):
+    for i in range(after, len(lines)):
+        if pat in lines[i]:
+            return i + 1
+    raise SystemExit("pattern not found: " + pat)
+
+
+def regions(lines):
+    """Sub-regions of the three large functions by anchor comments/lines."""
+    F = {n: (s, e) for n, s, e in fn_ranges(lines)}
+    R = []
+    ks, ke = F["render_kernel"]
+    wl = find_line(lines, "while (alive) {", ks)
+    body = [
+        ("kernel: prologue (grid copy, pool start)", ks, wl - 1),
+        ("step: head (pool ballot, mbcnt)", wl, find_line(lines, "if (tracing && best < 0) {", wl) - 1),
+        ("step: miss -> sky sum", find_line(lines, "if (tracing && best < 0) {", wl), find_line(lines, "if (miss) {", wl) - 1),
+        ("step: pool take", find_line(lines, "if (miss) {", wl), find_line(lines, "const uint4 r = pcg4d(pix", wl) - 1),
+        ("step: hash + polar draw", find_line(lines, "const uint4 r = pcg4d(pix", wl), find_line(lines, "if (!miss) {", wl) - 1),
+        ("hit: record load, refine, skip test", find_line(lines, "if (!miss) {", wl), find_line(lines, "const float px = fmaf(t, dx, ox)", wl) - 1),
+        ("hit: point, normal, reflect", find_line(lines, "const float px = fmaf(t, dx, ox)", wl), find_line(lines, "if (kind == RT_LAMBERTIAN) {", wl) - 1),
+        ("hit: lambertian", find_line(lines, "if (kind == RT_LAMBERTIAN) {", wl), find_line(lines, "if (kind == RT_METAL) {", wl) - 1),
+        ("hit: metal", find_line(lines, "if (kind == RT_METAL) {", wl), find_line(lines, "if (kind >= RT_DIELECTRIC) {", wl) - 1),
+        ("hit: dielectric", find_line(lines, "if (kind >= RT_DIELECTRIC) {", wl), find_line(lines, "thr *= sr.ar;", wl) - 1),
+        ("hit: attenuation, depth, next origin", find_line(lines, "thr *= sr.ar;", wl), find_line(lines, "} else if (tracing) {", wl) - 1),
+        ("step: new camera ray", find_line(lines, "} else if (tracing) {", wl), find_line(lines, "if (path_done) tracing = false;", wl) - 1),
+        ("step: tail (normalize3, t_min)", find_line(lines, "if (path_done) tracing = false;", wl), find_line(lines, "const int lane = lane_now();", wl) - 1),
+        ("kernel: epilogue (sums out, counters)", find_line(lines, "const int lane = lane_now();", wl), ke),
+    ]
+    R += body
+    W = []
+    cs, ce = F["closest_hit"]
+    W += [
+        ("walk: per-ray terms, reciprocals", cs, find_line(lines, "if (GRID) {", find_line(lines, "if (GRID || p.layer_mode)", cs)) - 1),
+        ("scan-all fallback (a lane beyond oref)", find_line(lines, "if (scan_all) {", cs), find_line(lines, "} else {", find_line(lines, "if (scan_all) {", cs))),
+        ("extras: four sphere tests", find_line(lines, "if (GRID || p.layer_mode)", cs), find_line(lines, "const f2 tyl = fma2", cs) - 1),
+        ("walk: layer slab", find_line(lines, "const f2 tyl = fma2", cs), ce),
+    ]
+    gs, ge = F["grid_walk"]
+    loop = find_line(lines, "while (true) {", gs)
+    il = find_line(lines, "if (ip != ie) do {", loop)
+    W += [
+        ("grid: clip, DDA start", gs, loop - 1),
+        ("grid: DDA iteration (cell bounds, step)", loop, ge),
+        ("grid: item loop control", il, find_line(lines, "} while (ip != ie);", il)),
+    ]
+    for n, lab in (("scan_pairs", "scan-all fallback (a lane beyond oref)"),
+                   ("scan_extras", "extras: four sphere tests"), ("grid_item", "grid: item test"),
+                   ("candidate", "candidate root sequence")):
+        W.append((lab, F[n][0], F[n][1]))
+    return R, W
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--s", help="an existing -gline-tables-only .s of rt_kernel.hip")
+    ap.add_argument("--json")
+    a = ap.parse_args()
+    lines = open(SRC).read().split("\n")
+    path = a.s
+    if not path:
+        path = "/tmp/rt_kernel_regions.s"
+        cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off",
+               "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(PKG, "csrc"), "-fno-slp-vectorize",
+               "-gline-tables-only", "--cuda-device-only", "-S", "-o", path, SRC]
+        subprocess.run(cmd, check=True, cwd=PKG, stderr=subprocess.DEVNULL)
+    R, W = regions(lines)
+    F = {n: (b, e) for n, b, e in fn_ranges(lines)}
+    s = open(path).read().split("\n")
+    start = [i for i, l in enumerate(s) if l.startswith("_Z") and KEY in l.split(":")[0]][0]
+    end = [i for i in range(start, len(s)) if s[i].startswith(".Lfunc_end")][0]
+    chain = []
+    count = collections.defaultdict(lambda: [0, 0, 0, 0])
+    in_loop = {}
+    loopdepth = ""
+    for l in s[start:end]:
+        t = l.strip()
+        if t.startswith(".loc"):
+            # ".loc 0 1195 31 ... ; a:l:c @[ b:l:c @[ ... ] ]": innermost first
+            com = l.split(";", 1)[1] if ";" in l else ""
+            chain = [int(m.group(1)) for m in re.finditer(r"csrc/rt_kernel\.hip:(\d+):\d+", com)]
+            continue
+        m = re.match(r"^\.LBB\S+:\s*;\s*(.*)", l)
+        if m:
+            loopdepth = m.group(1)
+            continue
+        if not t or t.startswith(";") or t.startswith(".") or t.endswith(":"):
+            continue
+        op = t.split()[0]
+        k = 0 if op.startswith("v_") else 1 if op.startswith("s_") else 2 if op.startswith("ds_") else 3
+        name = "no source line (block joins, exec masks)"
+        if chain:
+            # the kernel body's region of the outermost frame; inside
+            # closest_hit, the innermost walk region
+            outer = [r for r in R if r[1] <= chain[-1] <= r[2]]
+            name = outer[0][0] if outer else name
+            if any(F["closest_hit"][0] <= ln <= F["closest_hit"][1] for ln in chain):
+                for j, ln in enumerate(chain):
+                    hit = [r for r in W if r[1] <= ln <= r[2]]
+                    if not hit:
+                        continue
+                    name = min(hit, key=lambda r: r[2] - r[1])[0]
+                    if name == "candidate root sequence":  # split by caller
+                        for ln2 in chain[j + 1:]:
+                            if F["grid_item"][0] <= ln2 <= F["grid_item"][1]:
+                                name = "grid: candidate root sequence"
+                                break
+                            if F["scan_extras"][0] <= ln2 <= F["scan_extras"][1]:
+                                name = "extras: candidate root sequences"
+                                break
+                            if F["scan_pairs"][0] <= ln2 <= F["scan_pairs"][1]:
+                                name = "scan-all fallback (a lane beyond oref)"
+                                break
+                    break
+                if name.startswith("extras") and find_line(lines, "scan_extras<OPEN, STATS, false>", 0) in chain:
+                    name = "extras: groups after the first (scenes with > 4 extras)"
+        count[name][k] += 1
+        d = re.search(r"Depth=(\d)", loopdepth)
+        in_loop[name] = max(in_loop.get(name, 0), int(d.group(1)) if d else 0)
+    tot = [sum(c[i] for c in count.values()) for i in range(4)]
+    order = [r[0] for r in R + W] + ["extras: groups after the first (scenes with > 4 extras)"]
+    order[order.index("candidate root sequence"):order.index("candidate root sequence") + 1] = [
+        "extras: candidate root sequences", "grid: candidate root sequence", "candidate root sequence"]
+    rows = sorted(count.items(), key=lambda kv: order.index(kv[0]) if kv[0] in order else 99)
+    print(f"{'region':44s} {'VALU':>5s} {'SALU':>5s} {'DS':>3s} {'MEM':>3s} loop-depth")
+    for n, c in rows:
+        print(f"{n:44s} {c[0]:5d} {c[1]:5d} {c[2]:3d} {c[3]:3d} {in_loop.get(n, 0)}")
+    print(f"{'total':44s} {tot[0]:5d} {tot[1]:5d} {tot[2]:3d} {tot[3]:3d}")
+    if a.json:
+        json.dump({"regions": {n: {"valu": c[0], "salu": c[1], "ds": c[2], "mem": c[3],
+                                   "max_loop_depth": in_loop.get(n, 0)} for n, c in rows},
+                   "total": {"valu": tot[0], "salu": tot[1], "ds": tot[2], "mem": tot[3]}},
+                  open(a.json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
