@@ -10,8 +10,9 @@ render_kernel<false,false,true,false,true,1,false> to the innermost frame of
 its `.loc` inlined-at chain that lies in a region of REGIONS below (functions
 of rt_kernel.hip or line ranges of the kernel body), helpers (dot3, fma2,
 sqrt_k, ...) counting for their caller's region.  Prints one row per region:
-static VALU, SALU, LDS, memory instructions and whether the region sits in the
-grid's DDA / item loops.
+static VALU, SALU, LDS, vector-memory, SMEM, branch and wait instructions (the
+SQ counters' classes: SQ_INSTS_SALU counts scalar ALU only) and the region's
+loop depth.
 
     python tools/isa_regions.py [--s existing.s] [--json out.json]
 """
@@ -115,7 +116,7 @@ def main():
     start = [i for i, l in enumerate(s) if l.startswith("_Z") and KEY in l.split(":")[0]][0]
     end = [i for i in range(start, len(s)) if s[i].startswith(".Lfunc_end")][0]
     chain = []
-    count = collections.defaultdict(lambda: [0, 0, 0, 0])
+    count = collections.defaultdict(lambda: [0] * 7)
     in_loop = {}
     loopdepth = ""
     for l in s[start:end]:
@@ -132,7 +133,13 @@ def main():
         if not t or t.startswith(";") or t.startswith(".") or t.endswith(":"):
             continue
         op = t.split()[0]
-        k = 0 if op.startswith("v_") else 1 if op.startswith("s_") else 2 if op.startswith("ds_") else 3
+        # classes as the SQ counters count them: VALU, SALU, LDS, vector memory,
+        # SMEM (s_load / s_buffer_load), branches, s_waitcnt / s_nop
+        k = (0 if op.startswith("v_") else
+             4 if op.startswith(("s_load", "s_buffer_load", "s_dcache")) else
+             5 if op.startswith(("s_branch", "s_cbranch")) else
+             6 if op.startswith(("s_waitcnt", "s_nop")) else
+             1 if op.startswith("s_") else 2 if op.startswith("ds_") else 3)
         name = "no source line (block joins, exec masks)"
         if chain:
             # the kernel body's region of the outermost frame; inside
@@ -162,19 +169,22 @@ def main():
         count[name][k] += 1
         d = re.search(r"Depth=(\d)", loopdepth)
         in_loop[name] = max(in_loop.get(name, 0), int(d.group(1)) if d else 0)
-    tot = [sum(c[i] for c in count.values()) for i in range(4)]
+    tot = [sum(c[i] for c in count.values()) for i in range(7)]
     order = [r[0] for r in R + W] + ["extras: groups after the first (scenes with > 4 extras)"]
     order[order.index("candidate root sequence"):order.index("candidate root sequence") + 1] = [
         "extras: candidate root sequences", "grid: candidate root sequence", "candidate root sequence"]
     rows = sorted(count.items(), key=lambda kv: order.index(kv[0]) if kv[0] in order else 99)
-    print(f"{'region':44s} {'VALU':>5s} {'SALU':>5s} {'DS':>3s} {'MEM':>3s} loop-depth")
+    hdr = ("VALU", "SALU", "LDS", "VMEM", "SMEM", "BR", "WAIT")
+    print(f"{'region':56s} " + " ".join(f"{h:>5s}" for h in hdr) + " loop-depth")
     for n, c in rows:
-        print(f"{n:44s} {c[0]:5d} {c[1]:5d} {c[2]:3d} {c[3]:3d} {in_loop.get(n, 0)}")
-    print(f"{'total':44s} {tot[0]:5d} {tot[1]:5d} {tot[2]:3d} {tot[3]:3d}")
+        print(f"{n:56s} " + " ".join(f"{x:5d}" for x in c) + f" {in_loop.get(n, 0)}")
+    print(f"{'total':56s} " + " ".join(f"{x:5d}" for x in tot))
     if a.json:
-        json.dump({"regions": {n: {"valu": c[0], "salu": c[1], "ds": c[2], "mem": c[3],
-                                   "max_loop_depth": in_loop.get(n, 0)} for n, c in rows},
-                   "total": {"valu": tot[0], "salu": tot[1], "ds": tot[2], "mem": tot[3]}},
+        keys = ("valu", "salu", "lds", "vmem", "smem", "branch", "wait")
+        json.dump({"classes": "SQ counter classes: valu, salu (scalar ALU only), lds, vmem, smem, branch, "
+                              "wait (s_waitcnt / s_nop)",
+                   "regions": {n: dict(zip(keys, c), max_loop_depth=in_loop.get(n, 0)) for n, c in rows},
+                   "total": dict(zip(keys, tot))},
                   open(a.json, "w"), indent=1)
 
 
