@@ -149,9 +149,12 @@ typedef struct {
  * uint32 sum, F = 31 - floor(log2(spp)); the frame holds sum * 2^-F.  A scene
  * with an albedo A > 1 (energy-creating, as the reference allows) uses 64-bit
  * sums: v is clamped at vcap = min(A^(max_depth-1), 2^24) and F = 62 -
- * floor(log2(spp)) - ceil(log2(vcap)); since vcap >= 2^24 > spp whenever the
- * clamp acts, a clamped sample alone makes its pixel white in write_color, so
- * only the fp32 sums of such saturated pixels differ from an unclamped sum.  q truncates
+ * floor(log2(spp)) - ceil(log2(vcap)).  A^(max_depth-1) bounds a sample's
+ * radiance in exact arithmetic; the fp32 throughput, a product of rounded
+ * factors, can exceed it by a few ulps, so below 2^24 the clamp may trim such a
+ * sample at the ulp level (the oracle applies the same clamp).  At 2^24 > spp a
+ * clamped sample alone makes its pixel white in write_color, so there only the
+ * fp32 sums of saturated pixels differ from an unclamped sum.  q truncates
  * for spp < 4096 (F >= 20: a bias below 2^-20 per sample, under 0.03 of a
  * tonemap level on the darkest visible pixel) and rounds stochastically for
  * 4096 <= spp < 2^24, trunc(x) + (frac(x) > u) with u a uniform draw keyed by

@@ -185,9 +185,11 @@ int sum_bits(int spp) {
 // with vcap = min(A^(max_depth - 1), 2^24) (rounded down to fp32), a sample's
 // radiance clamped at vcap, and F = 62 - floor(log2 spp) - ceil(log2 vcap)
 // (spp samples of at most vcap 2^F, +1 each for the dither, fit 64 bits; F >=
-// 14).  vcap >= 2^24 > spp whenever the clamp can act: a clamped sample alone
-// makes its pixel's mean >= 1, white in either write_color, so the image is
-// the reference's; only the fp32 sums of such pixels saturate.
+// 14).  A^(max_depth - 1) bounds the radiance in exact arithmetic; the fp32
+// throughput can exceed it by a few ulps, so below 2^24 the clamp may trim a
+// sample at the ulp level (the oracle clamps alike: same bits).  At vcap =
+// 2^24 > spp a clamped sample alone makes its pixel's mean >= 1, white in
+// either write_color; only the fp32 sums of such pixels saturate.
 struct sum_fmt {
   bool wide;
   int f;
