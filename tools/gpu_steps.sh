@@ -2,8 +2,9 @@
 # The one runner of every GPU session (round 5: the per-session scripts of
 # rounds 3-4 are gone).  Runs GPU steps in order, each under its own time
 # limit.  A step that fails normally (exit 1: a test failure) does not stop
-# the sequence; a crash, abort, fault or time-out (anything else non-zero) ends
-# it -- nothing more touches the GPU after that.
+# the sequence; a crash, abort, fault or time-out (anything else non-zero), or
+# a GPU fault the runtime prints in the step's log, ends it -- nothing more
+# touches the GPU after that.
 #   tools/gpu_steps.sh "name|seconds|command" ...
 # The argument list is written to gpurun_out/<first step>.steps, which is
 # committed under profiles/ with the logs it produced.
@@ -20,5 +21,11 @@ for spec in "$@"; do
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
     echo "== stopping: $name ended with $rc"
     exit $rc
+  fi
+  # a device fault the runtime reported (the process may still exit 0 or 1):
+  # nothing more touches the GPU
+  if grep -qE "HSA_STATUS_ERROR|Memory access fault|MEMORY_APERTURE_VIOLATION" "gpurun_out/$name.log"; then
+    echo "== stopping: $name reported a GPU fault"
+    exit 3
   fi
 done
