@@ -125,9 +125,16 @@ bool sphere_hit(const dsphere &s, d3 o, d3 d, double tmin, double tmax, dhit &re
   return true;
 }
 
+unsigned long long g_last_trapped = 0;  // rto_reference_trapped
+
 struct dworld {
   std::vector<dsphere> s;
   unsigned long long calls = 0;
+  // attribution only (rto_reference_trapped): the sealed spheres of the
+  // opaque-inside rule (sealed_of on the fp64 scene) and the segments the
+  // reference traces after a path's first hit on the inside of one
+  std::vector<uint8_t> sealed;
+  unsigned long long trapped = 0;
   // hittable_list.h:28-43
   bool hit(d3 o, d3 d, double tmin, double tmax, dhit &rec) {
     ++calls;
@@ -191,13 +198,16 @@ bool scatter(const dsphere &m, d3 din, const dhit &rec, rng64 &r, d3 &att, d3 &d
   return true;
 }
 
-// main.cc:12-30 (recursive)
-d3 ray_color(d3 o, d3 d, dworld &w, rng64 &r, int depth) {
+// main.cc:12-30 (recursive); trapped: the path has hit a sealed sphere from
+// inside (counted in w.trapped, nothing else changes)
+d3 ray_color(d3 o, d3 d, dworld &w, rng64 &r, int depth, bool trapped = false) {
   if (depth <= 0) return {0, 0, 0};
   dhit rec;
+  if (trapped) ++w.trapped;
   if (w.hit(o, d, 0.001, INFINITY, rec)) {
     d3 att, dir;
-    if (scatter(w.s[rec.obj], d, rec, r, att, dir)) return att * ray_color(rec.p, dir, w, r, depth - 1);
+    const bool in = trapped || (!w.sealed.empty() && w.sealed[rec.obj] && !rec.front);
+    if (scatter(w.s[rec.obj], d, rec, r, att, dir)) return att * ray_color(rec.p, dir, w, r, depth - 1, in);
     return {0, 0, 0};
   }
   d3 ud = unit(d);
@@ -380,6 +390,7 @@ struct kctx {
   const float *out0 = nullptr;  // ... indexed like the frame tile out0
   bool no_dither = false;   // ... and the format without stochastic rounding (truncation only)
   bool tmin_world = false;  // t_min in world units (the round-4 specification, RTO_OPT_TMIN_WORLD)
+  bool no_sealed = false;   // without the opaque-inside rule (RTO_OPT_NO_SEALED, attribution only)
 };
 
 // the sum format's dither draw (rt_kernel.hip dither_u): pcg4d keyed by the
@@ -638,7 +649,7 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
       // the opaque-inside rule: a sealed lambertian
       // sphere hit at its exiting root ends the path (in the reference's
       // arithmetic every later chord inside it is t = |r|, to the depth cap)
-      if (sc.kind[b] == RT_LAMBERTIAN && sc.sealed[b] && !near) scattered = false;
+      if (sc.kind[b] == RT_LAMBERTIAN && sc.sealed[b] && !near && !k.no_sealed) scattered = false;
       if (wide)  // albedos above 1: the throughput stays finite (the kernel's clamp)
         for (int a = 0; a < 3; ++a) th[a] = std::fmin(th[a], 0x1p100f);
       ++depth;
@@ -1073,6 +1084,19 @@ int reference_render_world(dworld &w, rng64 &r, d3 lookfrom, d3 lookat, double a
                            int width, double aspect, int spp, int max_depth, uint8_t *rgb_out,
                            unsigned long long *segments) {
   const int height = (int)(width / aspect);
+  {  // the sealed spheres (sealed_of's rule on the fp64 scene), for rto_reference_trapped
+    const size_t n = w.s.size();
+    std::vector<uint8_t> over(n, 0);
+    for (size_t i = 0; i < n; ++i)
+      for (size_t j = i + 1; j < n; ++j) {
+        const d3 e = w.s[i].c - w.s[j].c;
+        const double rs = std::fabs(w.s[i].r) + std::fabs(w.s[j].r);
+        if (dot(e, e) < rs * rs) over[i] = over[j] = 1;
+      }
+    w.sealed.assign(n, 0);
+    for (size_t i = 0; i < n; ++i)
+      w.sealed[i] = w.s[i].kind == RT_LAMBERTIAN && !over[i] && std::fabs(w.s[i].r) > 0.002 && w.s[i].r > 0;
+  }
   // camera.h:8-26
   const double pi = 3.1415926535897932385;
   double theta = 20.0 * pi / 180.0;
@@ -1106,9 +1130,12 @@ int reference_render_world(dworld &w, rng64 &r, d3 lookfrom, d3 lookat, double a
     }
   }
   if (segments) *segments = w.calls;
+  g_last_trapped = w.trapped;
   return 0;
 }
 }  // namespace
+
+unsigned long long rto_reference_trapped() { return g_last_trapped; }
 
 int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
                             float *out, double *exact, int opts, unsigned long long *segments,
@@ -1123,6 +1150,7 @@ int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, co
   k.out0 = out;
   k.no_dither = (opts & RTO_OPT_NO_DITHER) != 0;
   k.tmin_world = (opts & RTO_OPT_TMIN_WORLD) != 0;
+  k.no_sealed = (opts & RTO_OPT_NO_SEALED) != 0;
   if (exact) std::memset(exact, 0, 3 * sizeof(double) * (size_t)p->local_rows * (size_t)p->width);
   if (threads < 1) {
     // the machine's cores, but no more than OMP_NUM_THREADS (16 on the GPU

@@ -12,6 +12,11 @@ extern "C" {
  * width*height*3 tonemapped bytes, TOP row first (src/cpu/main.cc:109-123).
  * scene 0 = final random scene (main.cc:32-76), 1 = five-sphere book scene.
  * rgb_out == NULL: size query (fills *height_out). */
+/* Attribution only: segments the last rto_reference_render(_view) traced
+ * after a path's first hit on the inside of a sealed lambertian sphere (the
+ * opaque-inside rule's spheres), which the kernel's rule
+ * does not trace. */
+unsigned long long rto_reference_trapped(void);
 int rto_reference_render(int width, double aspect, int spp, int max_depth, int scene,
                          uint8_t *rgb_out, int *height_out, unsigned long long *segments);
 /* The same for any scene (the final scene's camera, src/cpu/main.cc:90-97;
@@ -34,8 +39,10 @@ int rto_kernel_render(const rt_scene_view *scene, const rt_camera *cam, const rt
  *                      (truncation at every spp: the round-2 format);
  *   RTO_OPT_TMIN_WORLD t_min = 0.001 in world units on the normalised ray (the
  *                      round-1..4 form) instead of 0.001 in units of the
- *                      unnormalised direction, as the reference tests it. */
-enum { RTO_OPT_NO_DITHER = 1, RTO_OPT_TMIN_WORLD = 2 };
+ *                      unnormalised direction, as the reference tests it;
+ *   RTO_OPT_NO_SEALED  without the opaque-inside rule:
+ *                      paths inside a sealed lambertian ball bounce on. */
+enum { RTO_OPT_NO_DITHER = 1, RTO_OPT_TMIN_WORLD = 2, RTO_OPT_NO_SEALED = 4 };
 int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
                             float *out, double *exact, int opts, unsigned long long *segments,
                             int threads);

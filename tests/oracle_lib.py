@@ -73,14 +73,17 @@ def reference_render_view(scene, width, aspect, spp, max_depth=50):
 # of the specification, for the tests that show why they changed
 RTO_OPT_NO_DITHER = 1
 RTO_OPT_TMIN_WORLD = 2
+RTO_OPT_NO_SEALED = 4
 
 
-def kernel_render(scene, cam, params, threads=0, tmin_world=False):
+def kernel_render(scene, cam, params, threads=0, tmin_world=False, no_sealed=False):
     """fp32 restatement of the kernel algorithm -> (float32 [rows, W, 3], segments).
     tmin_world: t_min 0.001 in world units on the normalised ray (the
-    round-1..4 specification) instead of the reference's unit, 0.001 |d|."""
-    if tmin_world:
-        out, _, segs = _kernel_render_opts(scene, cam, params, RTO_OPT_TMIN_WORLD, False, threads)
+    round-1..4 specification) instead of the reference's unit, 0.001 |d|.
+    no_sealed: without the opaque-inside rule (attribution only)."""
+    if tmin_world or no_sealed:
+        opts = (RTO_OPT_TMIN_WORLD if tmin_world else 0) | (RTO_OPT_NO_SEALED if no_sealed else 0)
+        out, _, segs = _kernel_render_opts(scene, cam, params, opts, False, threads)
         return out, segs
     v = scene.view()
     out = np.zeros((params.local_rows, params.width, 3), np.float32)

@@ -149,6 +149,34 @@ def test_kernel_algorithm_c0_bias_within_reference_stream_noise(rtow):
     assert abs(np.mean(segs) - rs.mean()) <= 4.0 * seg_sigma, (np.mean(segs), rs.mean(), seg_sigma)
 
 
+def test_opaque_inside_rule_segments_attribution(rtow):
+    """What the opaque-inside rule removes:
+    the reference's own arithmetic (the fp64 restatement, byte-identical to
+    src/cpu) traces only 5.5e-5 of C0's segments after a path's first hit on
+    the inside of a sealed lambertian sphere, while the kernel algorithm
+    without the rule traces 3.9e-4 there (paired seeds): its fp32 roots on
+    the r = 1000 ground put ~6x more paths inside sealed balls at contacts.
+    With the rule the kernel's segment count is the reference's within
+    4e-5.  Pinned: the reference's share below 1.5e-4, the kernel's drop
+    between 2.5e-4 and 5.5e-4 over 8 seeds."""
+    import ctypes
+    from oracle_lib import lib
+    L = lib()
+    L.rto_reference_trapped.restype = ctypes.c_ulonglong
+    _, ref_segs = reference_render(400, 16.0 / 9.0, 10)
+    ref_share = L.rto_reference_trapped() / ref_segs
+    scene = rtow.final_scene()
+    cam = rtow.camera_cpu(aspect=400 / 225)
+    drop = []
+    for seed in range(8):
+        p = rtow.make_params(400, 225, 10, seed=seed)
+        drop.append(kernel_render(scene, cam, p, no_sealed=True)[1] - kernel_render(scene, cam, p)[1])
+    k_share = np.mean(drop) / ref_segs
+    print("reference trapped share %.2e, kernel rule drop %.2e" % (ref_share, k_share))
+    assert 0 < ref_share < 1.5e-4
+    assert 2.5e-4 < k_share < 5.5e-4
+
+
 def test_metal_fuzz_above_one_is_clamped(rtow):
     """rt_scene_upload (and the oracle's kernel mode) clamp metal fuzz to 1 as
     the reference's metal constructors do (src/cpu/material.h:38,
