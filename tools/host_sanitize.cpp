@@ -59,6 +59,18 @@ int main() {
     CHECK(rt_scene_final(he, &b, &next) == RT_OK);
     CHECK(b.n <= cap);
     accel(s.view(b.n), he >= 11);
+    // the grid fitter (RT_OPT_GRID_FIT's host model) for two frame geometries
+    if (he == 11 || he == 50) {
+      rt_camera cam;
+      const double from[3] = {13, 2, 3}, at[3] = {0, 0, 0}, up[3] = {0, 1, 0};
+      CHECK(rt_camera_cpu(from, at, up, 20.0, 16.0 / 9.0, 0.1, 10.0, &cam) == RT_OK);
+      const rt_scene_view v = s.view(b.n);
+      double scale = -1, costs[2 * 40];
+      size_t n = 0;
+      CHECK(rt_internal_grid_fit(&v, &cam, 3840, 2160, &scale, costs, 40, &n) == RT_OK);
+      CHECK(scale > 0 && n >= 1 && n <= 31);
+      CHECK(rt_internal_grid_fit(&v, &cam, 64, 64, &scale, nullptr, 0, &n) == RT_OK);
+    }
   }
   {  // too small a buffer is refused
     scene s;
