@@ -238,8 +238,9 @@ typedef enum {
   RT_OPT_BVH_COLLAPSE = 4,    /* BVH node collapse area ratio (default 0.35) */
   RT_OPT_BVH_SIDE = 5,        /* SAH weight of the x- and z-facing sides (default 1) */
   /* about this many samples (pixels x samples per pixel) per render kernel
-   * launch at most (default 2^32): a render is split into launches that each
-   * stay well under a second (no monolithic launch).  The render's
+   * launch at most (default 2^35, ~1.2 s at C4's density; 2^32 until round
+   * 5): a render is split into launches of bounded length (no
+   * monolithic launch; a C4 frame on one GPU runs as 16).  The render's
    * work entries (4-tile blocks x units) are first split by samples: `chunks`
    * launches over every entry, each tracing spp / chunks samples per pixel.
    * When that would leave a wave fewer than 100 samples per pixel, the
@@ -373,7 +374,7 @@ int rt_internal_accel_info(const rt_scene_view *scene, int grid_placement, doubl
 
 /* Host only (no device): how rt_render would cut a render with these
  * parameters into launches under a launch-sample budget (0 = the default,
- * 2^32; see RT_OPT_LAUNCH_SAMPLES).  Writes min(n_out, RT_LAUNCH_PLAN_N)
+ * 2^35; see RT_OPT_LAUNCH_SAMPLES).  Writes min(n_out, RT_LAUNCH_PLAN_N)
  * values: 0 block ranges, 1 sample ranges per block range, 2 units (waves per
  * tile), 3 work entries (blocks x units), 4 launches (ranges x sample ranges).
  * For tests. */

@@ -58,6 +58,7 @@ struct options {
   std::string gather = "auto";  // auto: rccl when gpus > 1
   std::string out;
   bool p6 = false, quiet = false;
+  double launch_samples = 0.0;  // RT_OPT_LAUNCH_SAMPLES (0: the library's default)
 };
 
 [[noreturn]] void die(const char *what, int st) {
@@ -74,7 +75,8 @@ void check(int st, const char *what) {
                "usage: %s [--width N] [--height N] [--spp N] [--depth N] [--seed N]\n"
                "          [--spheres HALF_EXTENT] [--scene final|five] [--camera cpu|gpu]\n"
                "          [--semantics cpu|gpu] [--accel bvh|scan] [--gpus N] [--device N]\n"
-               "          [--devices D0,D1,...] [--gather rccl|host] [--out FILE] [--p6] [--quiet]\n",
+               "          [--devices D0,D1,...] [--gather rccl|host] [--out FILE] [--p6] [--quiet]\n"
+               "          [--launch-samples N]\n",
                argv0);
   std::exit(2);
 }
@@ -131,6 +133,7 @@ int main(int argc, char **argv) {
     else if (a == "--out") o.out = next();
     else if (a == "--p6") o.p6 = true;
     else if (a == "--quiet") o.quiet = true;
+    else if (a == "--launch-samples") o.launch_samples = std::atof(next());
     else usage(argv[0]);
   }
   if (!height_set && (o.width != (gpu_mode ? 1920 : 1200))) {
@@ -236,6 +239,8 @@ int main(int argc, char **argv) {
   std::vector<rt_context *> ctxs(o.gpus, nullptr);
   for (int g = 0; g < o.gpus; ++g) {
     check(rt_context_create(jobs[g].device, &ctxs[g]), "rt_context_create");
+    if (o.launch_samples > 0.0)
+      check(rt_context_set_option(ctxs[g], RT_OPT_LAUNCH_SAMPLES, o.launch_samples), "rt_context_set_option");
     check(rt_scene_upload(ctxs[g], &view), "rt_scene_upload");
   }
   const bool use_rccl = o.gather == "rccl" || (o.gather == "auto" && o.gpus > 1);

@@ -49,13 +49,16 @@ constexpr int kUnits = 8;  // without the pilot
 constexpr int kCounterSlots = 32;
 // Bounded launches (failure detection): a render is split into
 // launches of about this many samples at most (RT_OPT_LAUNCH_SAMPLES
-// overrides).  2^32 keeps the headline frame (4.15e9 samples, ~0.13 s) and a
-// C3 rank share in one launch and cuts a C4 rank share (6.7e10) into 16
-// sample ranges of 125 spp.  When sample ranges alone would leave fewer than
-// kMinPoolSpp samples per pixel per wave, the work entries are split into
-// strided ranges as well and the samples into chunks of ~kPoolSpp
-// (rt_api.cpp plan_launches).  At most kMaxLaunches launches per render.
-constexpr double kLaunchSamples = 4294967296.0;
+// overrides).  2^35 (round 5; 2^32 before) keeps the headline frame (4.15e9
+// samples, ~0.12 s) and a C3 rank share in one launch and cuts a C4 rank
+// share (6.7e10) into 2 sample ranges of 1 000 spp (~1.2 s each): a wave's
+// longer sample pool idles fewer lanes at its tail, C4's share 2.40 -> 2.36 s
+// and C3's whole frame 921 -> 911 ms against 2^32.  When
+// sample ranges alone would leave fewer than kMinPoolSpp samples per pixel
+// per wave, the work entries are split into strided ranges as well and the
+// samples into chunks of ~kPoolSpp (rt_api.cpp plan_launches).  At most
+// kMaxLaunches launches per render.
+constexpr double kLaunchSamples = 34359738368.0;
 constexpr double kMinPoolSpp = 100.0;
 constexpr double kPoolSpp = 250.0;
 constexpr long long kMaxLaunches = 65536;

@@ -394,8 +394,8 @@ def test_bounded_launches_give_the_same_image(rtow, gpu_ctx):
     samples each (float stores, no atomics); with 2 units per tile and a
     2.0e8 budget as 3; with a 2^24 budget as 32.  Every image and segment
     count equals the one-launch render bit for bit.  At the default budget
-    (2^32) the headline frame (3840x2160x500 = 4.15e9 samples) stays one
-    launch, and C4's full share at 2000 spp (6.7e10) is 16 sample ranges
+    (2^35) the headline frame (3840x2160x500 = 4.15e9 samples) stays one
+    launch, and C4's full share at 2000 spp (6.7e10) is 2 sample ranges
     (test_host.py test_launch_plan)."""
     scene = rtow.final_scene(half_extent=50)
     gpu_ctx.upload(scene)

@@ -217,16 +217,23 @@ def test_abi_exports_every_declared_symbol(rtow):
     # headline frame (4.15e9 samples) and C1: one launch
     (3840, 2160, 500, 1, 0, (1, 1, 1, 32400)),
     (1920, 1080, 100, 1, 0, (1, 1, 4, 32400)),
-    # C3 and C4 rank shares (1/8): C3 one launch, C4 16 sample ranges of 125 spp
+    # C3 and C4 rank shares (1/8) at the default budget (2^35): C3 one
+    # launch, C4 2 sample ranges of 1 000 spp
     (7680, 4320, 1000, 8, 0, (1, 1, 2, 32640)),
-    (16384, 16384, 2000, 8, 0, (1, 16, 1, 131072)),
-    # whole C3 frame on one GPU: 8 sample ranges of 125 spp
-    (7680, 4320, 1000, 1, 0, (1, 8, 1, 129600)),
-    # whole C4 frame on one GPU: sample ranges alone would leave 16 spp per
-    # wave; 16 strided entry ranges x 8 sample ranges of 250 spp instead
-    (16384, 16384, 2000, 1, 0, (16, 8, 1, 1048576)),
-    # the CLI's progress test: 1080p at 2100 spp, 2 sample ranges of 1050 spp
-    (1920, 1080, 2100, 1, 0, (1, 2, 4, 32400)),
+    (16384, 16384, 2000, 8, 0, (1, 2, 1, 131072)),
+    # ... and at round 4's 2^32: C4's share 16 sample ranges of 125 spp
+    (16384, 16384, 2000, 8, 1 << 32, (1, 16, 1, 131072)),
+    # whole C3 frame on one GPU: one launch (8 sample ranges of 125 spp at 2^32)
+    (7680, 4320, 1000, 1, 0, (1, 1, 1, 129600)),
+    (7680, 4320, 1000, 1, 1 << 32, (1, 8, 1, 129600)),
+    # whole C4 frame on one GPU: 16 sample ranges of 125 spp; at 2^32 sample
+    # ranges alone would leave 16 spp per wave: 16 strided entry ranges x 8
+    # sample ranges of 250 spp instead
+    (16384, 16384, 2000, 1, 0, (1, 16, 1, 1048576)),
+    (16384, 16384, 2000, 1, 1 << 32, (16, 8, 1, 1048576)),
+    # the CLI's progress test: 1080p at 2100 spp with a 2^32 budget, 2 sample
+    # ranges of 1050 spp
+    (1920, 1080, 2100, 1, 1 << 32, (1, 2, 4, 32400)),
     # a small frame at 50 spp over the budget: 5 entry ranges, all 50 samples each
     (320, 180, 50, 1, 320 * 180 * 10, (5, 1, 1, 230)),
     # C4's share at 16 spp and a 2^24 budget: 32 entry ranges
@@ -248,7 +255,7 @@ def test_launch_plan(rtow, w, h, spp, world, budget, plan):
     assert got["launches"] == got["ranges"] * got["chunks"] <= 65536
     samples = w * h * spp / world
     if got["launches"] > 1:  # each launch within the budget (up to padding pixels)
-        assert samples / got["launches"] <= max(budget or 2 ** 32, samples / 65536) * 1.01
+        assert samples / got["launches"] <= max(budget or 2 ** 35, samples / 65536) * 1.01
 
 
 def test_invalid_arguments_return_status(rtow):

@@ -352,8 +352,10 @@ def test_cli_reports_each_device_and_refuses_missing_gpus(rtow):
     n = rtow.device_count()
     bad = subprocess.run(args + ["--gpus", str(n + 1)], capture_output=True, timeout=120, text=True)
     assert bad.returncode == 2 and f"only {n} HIP device" in bad.stderr
-    # a render long enough for several bounded launches reports its progress
-    big = [exe, "--width", "1920", "--height", "1080", "--spp", "2100", "--seed", "5", "--out", os.devnull]
+    # a render cut into several bounded launches reports its progress (a 2^32
+    # budget, --launch-samples: the default 2^35 keeps this frame one launch)
+    big = [exe, "--width", "1920", "--height", "1080", "--spp", "2100", "--seed", "5", "--out", os.devnull,
+           "--launch-samples", "4294967296"]
     r = subprocess.run(big, capture_output=True, timeout=120, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "Launches remaining: 0" in r.stderr and re.search(r"render [0-9.]+ ms in 2 launch", r.stderr), r.stderr

@@ -37,11 +37,15 @@ def main():
     ap.add_argument("--units", type=int, default=0, help="rt_params.units (0: automatic)")
     ap.add_argument("--grid-scale", type=float, default=0.0)
     ap.add_argument("--row-block", type=int, default=8, help="rows per interleaved band")
+    ap.add_argument("--launch-samples", type=float, default=0.0,
+                    help="RT_OPT_LAUNCH_SAMPLES, the launch budget in samples (0: the default 2^35)")
     a = ap.parse_args()
     import rtow
     w, h, spp, half = bench.PRESETS[a.preset]
     spp = a.spp or spp
     ctx = rtow.Context(0)
+    if a.launch_samples:
+        ctx.set_option(rtow.RT_OPT_LAUNCH_SAMPLES, a.launch_samples)
     t = time.perf_counter()
     scene = rtow.final_scene(half_extent=half)
     ctx.upload(scene, grid_mode=a.grid_mode, grid_scale=a.grid_scale)
