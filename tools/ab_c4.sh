@@ -3,6 +3,7 @@
 # pixel (default 200) for alternative librtow builds (GPU box):
 #   tools/ab_c4.sh <name> ...   (build/variants/<name>.so; "base" = the in-tree build)
 # base runs first and last to bracket drift.
+# (.gpurunignore keeps build/variants off the GPU box: drop that line for an A/B call.)
 set -e
 spp=${SPP:-200}
 run() {

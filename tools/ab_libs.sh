@@ -2,6 +2,7 @@
 # A/B kernel time of alternative librtow builds on the headline frame (GPU box):
 #   tools/ab_libs.sh <name> ...   (build/variants/<name>.so; "base" = the in-tree build)
 # Runs base first and last to bracket drift; each run checks the image sha256.
+# (.gpurunignore keeps build/variants off the GPU box: drop that line for an A/B call.)
 set -e
 mkdir -p gpurun_out
 run() {

@@ -12,7 +12,9 @@ build, each in its own process (a process loads one librtow):
     python tools/step_budget.py [--spp 100]        # prints one JSON line
 
 The per-wave-step instruction budget in DESIGN.md §8 is these counts times
-the static region counts of tools/isa_regions.py.
+the static region counts of tools/isa_regions.py.  count1 / count2 are built
+by tools/build_variant.sh with -DRT_COUNT_ITEMS=1 / 2 (.gpurunignore keeps
+build/variants off the GPU box: drop that line for the call that runs this).
 """
 import argparse
 import json
