@@ -4,7 +4,9 @@
 build, each in its own process (a process loads one librtow):
 
   base   (RT_COUNT_ITEMS=0): box_hits = wave-level DDA iterations,
-         roots = wave-level extras root sequences (LEAD + compacted rounds)
+         roots = extras root sequences (LEAD + compacted rounds), counted by
+         every lane the wave runs them for: / 64 ~ wave-level when the pool
+         keeps all lanes busy (lane efficiency ~0.99)
   count1 (RT_COUNT_ITEMS=1): box_hits = wave-level grid item iterations
   count2 (RT_COUNT_ITEMS=2): box_hits = wave-level item iterations with a
          candidate (the grid's root sequences)
@@ -58,7 +60,8 @@ def main():
     print(json.dumps({"workload": f"3840x2160x{a.spp} final scene, grid build", "segments": b["segments"],
                       "wave_steps": ws, "segments_per_wave_step": round(b["segments"] / ws, 2),
                       "per_wave_step": {"dda_iters": round(b["box_hits"] / ws, 3),
-                                        "extras_root_seqs": round(b["roots"] / ws, 3),
+                                        "extras_root_seqs_lane_summed": round(b["roots"] / ws, 3),
+                                        "extras_root_seqs_wave_approx": round(b["roots"] / ws / 64, 3),
                                         "item_iters": round(r["count1"]["box_hits"] / ws, 3),
                                         "grid_candidate_seqs": round(r["count2"]["box_hits"] / ws, 3),
                                         "lane_cells": round(b["lane_cells"] / ws, 2)}}), flush=True)
