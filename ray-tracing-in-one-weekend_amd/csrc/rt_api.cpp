@@ -329,9 +329,12 @@ int rt_scene_upload(rt_context *c, const rt_scene_view *s) {
   rtk::build_accel(s, o, a, c->grid_fit && !c->grid_scale_set ? &fitter : nullptr);
 
   RT_HIP(hipSetDevice(c->device));
-  // renders enqueued on caller streams may still read the old scene
+  // renders enqueued on caller streams may still read the old scene: they
+  // are serialised and each ends by recording ev_done, so the last one's
+  // event covers them all (this context's work only, not the whole device)
   {
-    const hipError_t e0 = hipDeviceSynchronize();
+    hipError_t e0 = c->have_done ? hipEventSynchronize(c->ev_done) : hipSuccess;
+    if (e0 == hipSuccess) e0 = hipStreamSynchronize(c->stream);
     if (e0 != hipSuccess) {
       delete fitter;
       return hip_fail(e0);
