@@ -126,6 +126,13 @@ bool sphere_hit(const dsphere &s, d3 o, d3 d, double tmin, double tmax, dhit &re
 }
 
 unsigned long long g_last_trapped = 0;  // rto_reference_trapped
+// kernel mode, attribution only (rto_kernel_attrib): spurious-root skips,
+// first hits on the inside of a sealed sphere, and those of them whose ray
+// had just been moved on by a skip
+std::atomic<unsigned long long> g_skips{0}, g_inner{0}, g_inner_after_skip{0};
+// ... and the first 4096 entries: (sphere entered, previous segment's sphere, depth, t_min * 1e6)
+std::atomic<unsigned> g_ev_n{0};
+long long g_ev[4096][4];
 
 struct dworld {
   std::vector<dsphere> s;
@@ -391,6 +398,8 @@ struct kctx {
   bool no_dither = false;   // ... and the format without stochastic rounding (truncation only)
   bool tmin_world = false;  // t_min in world units (the round-4 specification, RTO_OPT_TMIN_WORLD)
   bool no_sealed = false;   // without the opaque-inside rule (RTO_OPT_NO_SEALED, attribution only)
+  bool fp64_roots = false;  // candidates' roots in fp64 (RTO_OPT_FP64_ROOTS, attribution only)
+  bool same_exit = true;    // the same-sphere exit rule (RTO_OPT_NO_SAME_EXIT turns it off)
 };
 
 // the sum format's dither draw (rt_kernel.hip dither_u): pcg4d keyed by the
@@ -467,6 +476,9 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
     float o[3], d[3];
     float tmin = camera_ray(k, pix, col, grow, sample, o, d);
     float th[3] = {1.0f, 1.0f, 1.0f};
+    bool after_skip = false, inner_seen = false;  // rto_kernel_attrib
+    long prev_best = -2;
+    long origin_sphere = -1;  // the sphere the ray starts on (-1: a camera ray)
     for (int depth = 0;;) {
       ++segs;
       // closest hit: expanded quadratic with |d| = 1
@@ -508,7 +520,18 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
             // interval, first for the open src/gpu one -- what a sequential scan
             // does, stated so that any visiting order gives the same winner)
             const float sq = sqrt_k(eb[j]);
-            const float t0 = h - sq, t1 = h + sq;
+            float t0 = h - sq, t1 = h + sq;
+            if (k.fp64_roots) {  // the same ray and sphere, roots in fp64
+              const double ocx = (double)o[0] - sc.cx[i], ocy = (double)o[1] - sc.cy[i], ocz = (double)o[2] - sc.cz[i];
+              const double b = ocx * d[0] + ocy * d[1] + ocz * d[2];
+              const double r = sc.radius[i];
+              const double c = ocx * ocx + ocy * ocy + ocz * ocz - r * r;
+              const double dd = b * b - c;
+              if (!(dd >= 0.0)) continue;
+              const double s = std::sqrt(dd);
+              t0 = (float)(-b - s);
+              t1 = (float)(-b + s);
+            }
             const bool use0 = k.open ? t0 > tmin : t0 >= tmin;
             const float root = use0 ? t0 : t1;
             const bool above = k.open ? root > tmin : root >= tmin;
@@ -566,12 +589,21 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
         // arithmetic it cannot meet again (src/cpu, fp64, never does at
         // t >= 0.001); the expanded quadratic's root was an fp32 artefact (for
         // spheres far from the origin it can trap the path inside the
-        // sphere).  Not a segment: the ray moves on to the scan's root point
-        // (>= t_min further, so this ends) and walks again, same direction.
-        // (the ray keeps its t_min: same direction, same parameter unit)
-        if (t < tmin && bb > 0.0f) {
+        // sphere).  So is (round 5) the exiting root of the sphere the ray
+        // starts on when it moves away from that sphere's centre: t = 0 in
+        // exact arithmetic, an fp32 hit point an ulp inside the ball with a
+        // tiny t_min (lambertian n + u, u ~ -n) otherwise.  Not a segment: the
+        // ray moves on to the scan's root point and walks again, same
+        // direction.  (the ray keeps its t_min: same direction, same unit)
+        if (bb > 0.0f && (t < tmin || (k.same_exit && best == origin_sphere && !near))) {
           if (tr) std::fprintf(g_trace, "  spurious best %ld t %.9g: skipped\n", best, tmax);
-          for (int a = 0; a < 3; ++a) o[a] = fmaf_(tmax, d[a], o[a]);
+          g_skips.fetch_add(1, std::memory_order_relaxed);
+          after_skip = true;
+          if (t < tmin) {
+            for (int a = 0; a < 3; ++a) o[a] = fmaf_(tmax, d[a], o[a]);
+          } else {  // the same origin, t_min just past the scan's root (the kernel's bit step)
+            tmin = std::nextafter(tmax, INFINITY);
+          }
           normalize3(d[0], d[1], d[2]);
           --segs;
           continue;
@@ -649,6 +681,20 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
       // the opaque-inside rule: a sealed lambertian
       // sphere hit at its exiting root ends the path (in the reference's
       // arithmetic every later chord inside it is t = |r|, to the depth cap)
+      if (sc.kind[b] == RT_LAMBERTIAN && sc.sealed[b] && !near && !inner_seen) {
+        inner_seen = true;
+        g_inner.fetch_add(1, std::memory_order_relaxed);
+        if (after_skip) g_inner_after_skip.fetch_add(1, std::memory_order_relaxed);
+        const unsigned e = g_ev_n.fetch_add(1);
+        if (e < 4096) {
+          g_ev[e][0] = (long long)b;
+          g_ev[e][1] = prev_best;
+          g_ev[e][2] = depth;
+          g_ev[e][3] = (long long)(tmin * 1e6f);
+        }
+      }
+      prev_best = (long)b;
+      after_skip = false;
       if (sc.kind[b] == RT_LAMBERTIAN && sc.sealed[b] && !near && !k.no_sealed) scattered = false;
       if (wide)  // albedos above 1: the throughput stays finite (the kernel's clamp)
         for (int a = 0; a < 3; ++a) th[a] = std::fmin(th[a], 0x1p100f);
@@ -658,6 +704,7 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
         o[a] = p[a];
         d[a] = sd[a];
       }
+      origin_sphere = (long)b;
       tmin = tmin_of(k.tmin_world, normalize3(d[0], d[1], d[2]));
     }
   }
@@ -1137,6 +1184,20 @@ int reference_render_world(dworld &w, rng64 &r, d3 lookfrom, d3 lookat, double a
 
 unsigned long long rto_reference_trapped() { return g_last_trapped; }
 
+void rto_kernel_attrib(unsigned long long *out, int reset) {
+  out[0] = g_skips.load();
+  out[1] = g_inner.load();
+  out[2] = g_inner_after_skip.load();
+  if (reset) g_skips = g_inner = g_inner_after_skip = 0;
+}
+
+int rto_kernel_attrib_events(long long *out, int n, int reset) {
+  const int m = (int)std::min<unsigned>(g_ev_n.load(), std::min(n, 4096));
+  std::memcpy(out, g_ev, sizeof(long long) * 4 * (size_t)m);
+  if (reset) g_ev_n = 0;
+  return m;
+}
+
 int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
                             float *out, double *exact, int opts, unsigned long long *segments,
                             int threads) {
@@ -1151,6 +1212,8 @@ int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, co
   k.no_dither = (opts & RTO_OPT_NO_DITHER) != 0;
   k.tmin_world = (opts & RTO_OPT_TMIN_WORLD) != 0;
   k.no_sealed = (opts & RTO_OPT_NO_SEALED) != 0;
+  k.fp64_roots = (opts & RTO_OPT_FP64_ROOTS) != 0;
+  k.same_exit = (opts & RTO_OPT_NO_SAME_EXIT) == 0;
   if (exact) std::memset(exact, 0, 3 * sizeof(double) * (size_t)p->local_rows * (size_t)p->width);
   if (threads < 1) {
     // the machine's cores, but no more than OMP_NUM_THREADS (16 on the GPU

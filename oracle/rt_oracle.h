@@ -17,6 +17,14 @@ extern "C" {
  * opaque-inside rule's spheres), which the kernel's rule
  * does not trace. */
 unsigned long long rto_reference_trapped(void);
+/* Attribution only: kernel-mode counters summed over every render since the
+ * last reset: out[0] spurious-root skips, out[1] paths' first hits on the
+ * inside of a sealed sphere, out[2] those whose ray had just been moved on by
+ * a skip.  reset != 0 zeroes them after reading. */
+void rto_kernel_attrib(unsigned long long *out, int reset);
+/* ... the first entries' (sphere entered, previous segment's sphere, depth,
+ * t_min * 1e6), at most n of them (and 4096); returns how many. */
+int rto_kernel_attrib_events(long long *out, int n, int reset);
 int rto_reference_render(int width, double aspect, int spp, int max_depth, int scene,
                          uint8_t *rgb_out, int *height_out, unsigned long long *segments);
 /* The same for any scene (the final scene's camera, src/cpu/main.cc:90-97;
@@ -41,8 +49,15 @@ int rto_kernel_render(const rt_scene_view *scene, const rt_camera *cam, const rt
  *                      round-1..4 form) instead of 0.001 in units of the
  *                      unnormalised direction, as the reference tests it;
  *   RTO_OPT_NO_SEALED  without the opaque-inside rule:
- *                      paths inside a sealed lambertian ball bounce on. */
-enum { RTO_OPT_NO_DITHER = 1, RTO_OPT_TMIN_WORLD = 2, RTO_OPT_NO_SEALED = 4 };
+ *                      paths inside a sealed lambertian ball bounce on;
+ *   RTO_OPT_FP64_ROOTS each candidate's roots (and so the t_min decision)
+ *                      from fp64 arithmetic on the fp32 ray and sphere
+ *                      (attribution only: is the fp32 root the cause?);
+ *   RTO_OPT_NO_SAME_EXIT without round 5's same-sphere exit rule (the exiting
+ *                      root of the sphere a ray starts on, moving away from
+ *                      its centre, taken as a hit: the round-4 form). */
+enum { RTO_OPT_NO_DITHER = 1, RTO_OPT_TMIN_WORLD = 2, RTO_OPT_NO_SEALED = 4, RTO_OPT_FP64_ROOTS = 8,
+       RTO_OPT_NO_SAME_EXIT = 16 };
 int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
                             float *out, double *exact, int opts, unsigned long long *segments,
                             int threads);

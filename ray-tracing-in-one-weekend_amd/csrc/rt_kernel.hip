@@ -911,6 +911,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   float thr = 1.f, thg = 1.f, thb = 1.f;
   int depth = 0;
   uint32_t slot = 0, sample = 0, pix = 0;
+  int origin_sphere = -1;  // the sphere the ray starts on (-1: a camera ray)
   uint32_t segs = 0, steps = 0;
   work_ctr wc;  // executed work, STATS builds only
   // take pool item k: slot, sample and pixel; false if the slot is outside the
@@ -1024,12 +1025,26 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         // A refined root before t_min on a sphere the ray moves away from
         // (b > 0): the ray starts on that sphere and leaves its ball, which it
         // cannot meet again; the expanded quadratic's root was an fp32 artefact
-        // (DESIGN.md 2, step 3).  Not a segment: the ray moves on to the
-        // scan's root point, same direction (and t_min), and walks again.
-        if (t < tmin && b > 0.0f) {
-          ox = fmaf(tmax, dx, ox);
-          oy = fmaf(tmax, dy, oy);
-          oz = fmaf(tmax, dz, oz);
+        // (DESIGN.md 2, step 3).  So is the exiting root of the very sphere
+        // the ray starts on when it moves away from its centre: in exact
+        // arithmetic that root is t = 0 (the origin is on the surface), but an
+        // fp32 hit point can sit inside the ball by an ulp, which a bounce
+        // with a tiny t_min (lambertian n + u with u ~ -n) then "exits" --
+        // 6x as many paths entered sealed balls as in the reference's fp64
+        // (DESIGN.md 2, step 4).  Not a segment: the ray walks again, same
+        // direction -- in the first case from the scan's root point (>= t_min
+        // further), in the second from the same origin with t_min raised just
+        // past the scan's root, so that root cannot be taken again (moving the
+        // origin instead can take ~t_exit / t_min re-walks, unbounded as
+        // |n + u| -> 0).
+        if (b > 0.0f && (t < tmin || (best == origin_sphere && !near))) {
+          if (t < tmin) {
+            ox = fmaf(tmax, dx, ox);
+            oy = fmaf(tmax, dy, oy);
+            oz = fmaf(tmax, dz, oz);
+          } else {
+            tmin = __uint_as_float(__float_as_uint(tmax) + 1u);  // nextafter(tmax, +inf), tmax > 0 finite
+          }
           skipped = true;
           --segs;
         } else {
@@ -1114,6 +1129,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           dx = sx;  // normalised below, with the new camera rays
           dy = sy;
           dz = sz;
+          origin_sphere = best;
         }
         }
       } else if (tracing) {
@@ -1122,6 +1138,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         pixel_cr(q, col, grow);
         camera_dir(q, r, ux, uy, col, grow, ox, oy, oz, dx, dy, dz);
         depth = 0;
+        origin_sphere = -1;
         thr = thg = thb = 1.0f;
       }
     }
