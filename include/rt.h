@@ -257,7 +257,13 @@ typedef enum {
    * k = 0..30, that fit the grid's LDS placement); 0: the builder's grid.
    * No fitting either when RT_OPT_GRID_SCALE is set (non-zero).  Set before
    * rt_scene_upload.  Scheduling only: every size renders the same image. */
-  RT_OPT_GRID_FIT = 7
+  RT_OPT_GRID_FIT = 7,
+  /* the layer grid's origin shifted by this fraction of a cell in x / z,
+   * [0, 1) (default 0: the grid starts at the layer's padded bounds).  Read by
+   * the next rt_scene_upload; applies to the fitter's candidates too.
+   * Scheduling only: every grid renders the same image. */
+  RT_OPT_GRID_PHASE_X = 8,
+  RT_OPT_GRID_PHASE_Z = 9
 } rt_option;
 enum { RT_GRID_AUTO = 0, RT_GRID_LDS = 1, RT_GRID_CELLS_LDS = 2, RT_GRID_GLOBAL = 3 };
 int rt_context_set_option(rt_context *ctx, int option, double value);
@@ -389,6 +395,11 @@ int rt_internal_launch_plan(const rt_params *params, double launch_samples, uint
  * For tests and tools. */
 int rt_internal_grid_fit(const rt_scene_view *scene, const rt_camera *cam, int width, int height, double *scale,
                          double *costs, size_t n_costs, size_t *n);
+/* The same with the grid's origin shifted by (phase_x, phase_z) cells, each
+ * in [0, 1) (RT_OPT_GRID_PHASE_X / _Z).  For tools. */
+int rt_internal_grid_fit_phase(const rt_scene_view *scene, const rt_camera *cam, int width, int height,
+                               double phase_x, double phase_z, double *scale, double *costs, size_t n_costs,
+                               size_t *n);
 /* The cell scale of the context's current layer grid (after RT_OPT_GRID_FIT
  * refits it for a render's frame geometry); 0 without a grid.  For tests and
  * the bench record. */

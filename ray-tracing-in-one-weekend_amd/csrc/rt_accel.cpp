@@ -43,6 +43,7 @@ struct bvh_builder {
   double collapse_area = 0.35;
   double side_weight = 1.0;  // SAH weight of the x- and z-facing sides
   double grid_scale = 1.0;   // layer-grid cell side multiplier
+  double grid_phase_x = 0.0, grid_phase_z = 0.0;  // grid origin shifted by these fractions of a cell, [0, 1)
 
   double area(const box &b) const {
     const double dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
@@ -294,7 +295,12 @@ struct bvh_builder {
     x1 += 2 * pad;
     z1 += 2 * pad;
     double g = grid_scale * std::sqrt((x1 - x0) * (z1 - z0) / (double)n_tree);
+    const double bx0 = x0, bz0 = z0;
     for (int attempt = 0; attempt < 8; ++attempt, g *= 0.8) {
+      // the phase moves the cell borders relative to the spheres (the image is
+      // the same for every grid)
+      x0 = bx0 - grid_phase_x * g;
+      z0 = bz0 - grid_phase_z * g;
       const int nx = (int)std::ceil((x1 - x0) / g), nz = (int)std::ceil((z1 - z0) / g);
       if ((long long)nx * nz > (1 << 20)) return;
       std::vector<std::vector<uint32_t>> lists((size_t)nx * nz);
@@ -531,6 +537,8 @@ void build_accel(const rt_scene_view *s, const accel_options &o, accel_build &a,
   bb.collapse_area = o.collapse;
   bb.side_weight = o.side;
   bb.grid_scale = o.grid_scale;
+  bb.grid_phase_x = o.grid_phase_x;
+  bb.grid_phase_z = o.grid_phase_z;
   bb.run(s);
   // Grid placement.  The whole grid in LDS when it fits the
   // per-block budget (u16 LDS addresses: < 4096 items); else, for auto or
@@ -649,6 +657,8 @@ grid_fitter *grid_fitter::make_from(const rt_scene_view *s, const accel_options 
     q->bb.collapse_area = o.collapse;
     q->bb.side_weight = o.side;
     q->bb.grid_scale = scale0;
+    q->bb.grid_phase_x = o.grid_phase_x;
+    q->bb.grid_phase_z = o.grid_phase_z;
     q->bb.run(&q->view);
   }
   q->placement = placement;

@@ -299,6 +299,11 @@ int rt_context_set_option(rt_context *c, int option, double v) {
       if (v != 0.0 && v != 1.0) return RT_ERR_INVALID;
       c->grid_fit = v != 0.0;
       return RT_OK;
+    case RT_OPT_GRID_PHASE_X:
+    case RT_OPT_GRID_PHASE_Z:
+      if (!(v >= 0.0 && v < 1.0)) return RT_ERR_INVALID;
+      (option == RT_OPT_GRID_PHASE_X ? c->opt.grid_phase_x : c->opt.grid_phase_z) = v;
+      return RT_OK;
     case RT_OPT_BVH_LEAF:
       if (v != std::floor(v) || v < 0 || v > 4) return RT_ERR_INVALID;
       c->opt.bvh_leaf = dflt ? 4 : (int)v;
@@ -918,8 +923,16 @@ int rt_internal_accel_info(const rt_scene_view *s, int grid_placement, double gr
 
 int rt_internal_grid_fit(const rt_scene_view *s, const rt_camera *cam, int width, int height, double *scale,
                          double *costs, size_t n_costs, size_t *n) {
+  return rt_internal_grid_fit_phase(s, cam, width, height, 0.0, 0.0, scale, costs, n_costs, n);
+}
+
+int rt_internal_grid_fit_phase(const rt_scene_view *s, const rt_camera *cam, int width, int height, double phase_x,
+                               double phase_z, double *scale, double *costs, size_t n_costs, size_t *n) {
   if (!rtk::scene_ok(s) || !cam || !scale || width < 1 || height < 1 || (n_costs && !costs)) return RT_ERR_INVALID;
+  if (!(phase_x >= 0.0 && phase_x < 1.0 && phase_z >= 0.0 && phase_z < 1.0)) return RT_ERR_INVALID;
   rtk::accel_options o;
+  o.grid_phase_x = phase_x;
+  o.grid_phase_z = phase_z;
   o.wide = rtk::max_albedo(s) > 1.0;
   rtk::accel_build a;
   rtk::grid_fitter *f = nullptr;

@@ -41,6 +41,7 @@ ABI_VERSION = 5
 # rt_context_set_option (include/rt.h): placement / shape / launch options, never semantics
 RT_OPT_GRID_PLACEMENT, RT_OPT_GRID_SCALE, RT_OPT_BVH_LEAF = 1, 2, 3
 RT_OPT_BVH_COLLAPSE, RT_OPT_BVH_SIDE, RT_OPT_LAUNCH_SAMPLES, RT_OPT_GRID_FIT = 4, 5, 6, 7
+RT_OPT_GRID_PHASE_X, RT_OPT_GRID_PHASE_Z = 8, 9
 RT_GRID_AUTO, RT_GRID_LDS, RT_GRID_CELLS_LDS, RT_GRID_GLOBAL = 0, 1, 2, 3
 GRID_PLACEMENTS = {"auto": RT_GRID_AUTO, "lds": RT_GRID_LDS, "cells": RT_GRID_CELLS_LDS, "global": RT_GRID_GLOBAL}
 
@@ -330,15 +331,19 @@ class Context:
         """rt_context_set_option: placement / shape / launch granularity (0 = default)."""
         check(lib().rt_context_set_option(self._h, option, float(value)), "rt_context_set_option")
 
-    def upload(self, scene, grid_mode=None, grid_scale=None):
+    def upload(self, scene, grid_mode=None, grid_scale=None, grid_phase=None):
         """rt_scene_upload; grid_mode ("auto", "lds", "cells", "global") and
-        grid_scale set the layer grid's options first (the image is the same).
+        grid_scale / grid_phase ((x, z) cell fractions) set the layer grid's
+        options first (the image is the same).
         Options are the context's: they stay set for later uploads until set
         again (0 / "auto" restores the default)."""
         if grid_mode is not None:
             self.set_option(RT_OPT_GRID_PLACEMENT, GRID_PLACEMENTS[grid_mode])
         if grid_scale is not None:
             self.set_option(RT_OPT_GRID_SCALE, grid_scale)
+        if grid_phase is not None:
+            self.set_option(RT_OPT_GRID_PHASE_X, grid_phase[0])
+            self.set_option(RT_OPT_GRID_PHASE_Z, grid_phase[1])
         v = scene.view()
         check(lib().rt_scene_upload(self._h, ctypes.byref(v)), "rt_scene_upload")
         self.scene = scene
@@ -423,19 +428,22 @@ def accel_info(scene, grid_mode="auto", grid_scale=0.0):
     return {k: int(x) for k, x in zip(ACCEL_INFO_KEYS, out)}
 
 
-def grid_fit(scene, cam, width, height):
+def grid_fit(scene, cam, width, height, phase=(0.0, 0.0)):
     """What RT_OPT_GRID_FIT picks for `scene` seen by `cam` in a width x height
-    frame, computed on the host (rt_internal_grid_fit; no device): (cell scale
-    or 0.0 without an LDS grid, [(candidate scale, modelled cost)])."""
+    frame, computed on the host (rt_internal_grid_fit_phase; no device), with
+    the grid origin shifted by `phase` cells (RT_OPT_GRID_PHASE_X / _Z): (cell
+    scale or 0.0 without an LDS grid, [(candidate scale, modelled cost)])."""
     L = lib()
-    L.rt_internal_grid_fit.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                                       ctypes.POINTER(ctypes.c_double), ctypes.c_void_p, ctypes.c_size_t,
-                                       ctypes.POINTER(ctypes.c_size_t)]
+    L.rt_internal_grid_fit_phase.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_double, ctypes.c_double,
+                                             ctypes.POINTER(ctypes.c_double), ctypes.c_void_p, ctypes.c_size_t,
+                                             ctypes.POINTER(ctypes.c_size_t)]
     v = scene.view()
     sc, n = ctypes.c_double(), ctypes.c_size_t()
     costs = np.zeros(2 * 64, np.float64)
-    check(L.rt_internal_grid_fit(ctypes.byref(v), ctypes.byref(cam), width, height, ctypes.byref(sc),
-                                 costs.ctypes.data, 64, ctypes.byref(n)), "rt_internal_grid_fit")
+    check(L.rt_internal_grid_fit_phase(ctypes.byref(v), ctypes.byref(cam), width, height, float(phase[0]),
+                                       float(phase[1]), ctypes.byref(sc), costs.ctypes.data, 64,
+                                       ctypes.byref(n)), "rt_internal_grid_fit_phase")
     return sc.value, [(float(costs[2 * i]), float(costs[2 * i + 1])) for i in range(min(64, n.value))]
 
 

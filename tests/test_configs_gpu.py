@@ -304,9 +304,10 @@ def test_c4_scene_at_2000spp_bit_exact_vs_oracle(rtow, gpu_ctx, oracle, mode, un
 def test_grid_cell_scales_render_the_oracle_image(rtow, gpu_ctx, oracle, half_extent):
     """The layer grid's cell size (RT_OPT_GRID_SCALE) is scheduling only: the
     headline scene (grid in LDS) and C4's (cells in LDS) uploaded at the
-    builder's scale s0 and at s0 (1 + 0.01 k), k = 3, 7, 15, 30, render the
-    oracle's image bit for bit with equal segments (the lists hold every
-    sphere that can win)."""
+    builder's scale s0 and at s0 (1 + 0.01 k), k = 3, 7, 15, 30, and with the
+    grid's origin shifted by a fraction of a cell (RT_OPT_GRID_PHASE_X / _Z),
+    render the oracle's image bit for bit with equal segments (the lists hold
+    every sphere that can win)."""
     scene = rtow.final_scene(half_extent=half_extent)
     W, H = (64, 36) if half_extent == 11 else (64, 64)
     cam = rtow.camera_cpu(aspect=W / H)
@@ -314,13 +315,16 @@ def test_grid_cell_scales_render_the_oracle_image(rtow, gpu_ctx, oracle, half_ex
     want, segs = kernel_render(scene, cam, p)
     s0 = rtow.accel_info(scene)["grid_scale_milli"] / 1000.0
     try:
-        for k in (0, 3, 7, 15, 30):
-            gpu_ctx.upload(scene, grid_mode="auto", grid_scale=s0 * (1.0 + 0.01 * k))
+        for k, ph in ((0, (0, 0)), (3, (0, 0)), (7, (0, 0)), (15, (0, 0)), (30, (0, 0)), (0, (0.5, 0.25)),
+                      (7, (0.75, 0.875))):
+            gpu_ctx.upload(scene, grid_mode="auto", grid_scale=s0 * (1.0 + 0.01 * k), grid_phase=ph)
             got, st = gpu_ctx.render(cam, p)
-            assert np.array_equal(got, want), (k, int((got != want).sum()))
-            assert st.segments == segs, k
+            assert np.array_equal(got, want), (k, ph, int((got != want).sum()))
+            assert st.segments == segs, (k, ph)
     finally:
         gpu_ctx.set_option(rtow.RT_OPT_GRID_SCALE, 0)
+        gpu_ctx.set_option(rtow.RT_OPT_GRID_PHASE_X, 0)
+        gpu_ctx.set_option(rtow.RT_OPT_GRID_PHASE_Z, 0)
 
 
 @pytest.mark.parametrize("spp", [1000, 2000, 2047, 4096])

@@ -203,7 +203,7 @@ def test_ppm_writer_p3_and_p6(rtow, tmp_path):
 def test_abi_exports_every_declared_symbol(rtow):
     hdr = open(os.path.join(ROOT, "include", "rt.h")).read()
     names = sorted(set(re.findall(r"^\s*(?:[\w\*\s]+?)\b(rt_\w+)\s*\(", hdr, re.M)))
-    assert len(names) == 27, names
+    assert len(names) == 28, names
     L = rtow.lib()
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
@@ -350,6 +350,26 @@ def test_grid_fit_picks_a_candidate_per_camera(rtow):
     up = rtow.camera_cpu(lookfrom=(0, 1, 0), lookat=(0, 5, 0.01), aspect=1.0)  # sky only
     assert rtow.grid_fit(fin, up, 64, 64)[0] == s0
     assert rtow.grid_fit(rtow.five_scene(), cam, 64, 36)[0] == 0.0
+
+
+def test_grid_phase_keeps_the_grid_invariants(rtow):
+    """RT_OPT_GRID_PHASE_X / _Z (the grid's origin shifted by a fraction of a
+    cell): the fitter's candidates at every phase are grids the
+    placement holds, the model's costs differ with the phase (the cell borders
+    move relative to the spheres) and phases outside [0, 1) are refused."""
+    fin = rtow.final_scene()
+    cam = rtow.camera_cpu(aspect=16 / 9)
+    base = rtow.grid_fit(fin, cam, 3840, 2160)
+    seen = set()
+    for ph in ((0.0, 0.0), (0.25, 0.25), (0.5, 0.0), (0.875, 0.125)):
+        sc, costs = rtow.grid_fit(fin, cam, 3840, 2160, ph)
+        assert len(costs) >= 20 and sc == min(costs, key=lambda x: x[1])[0]
+        seen.add(tuple(round(c, 9) for _, c in costs))
+    assert rtow.grid_fit(fin, cam, 3840, 2160, (0.0, 0.0)) == base
+    assert len(seen) == 4
+    for bad in ((1.0, 0.0), (0.0, -0.1)):
+        with pytest.raises(rtow.RTError):
+            rtow.grid_fit(fin, cam, 3840, 2160, bad)
 
 
 def test_accel_builder_on_degenerate_scenes(rtow):
