@@ -325,6 +325,9 @@ def test_grid_cell_scales_render_the_oracle_image(rtow, gpu_ctx, oracle, half_ex
         gpu_ctx.set_option(rtow.RT_OPT_GRID_SCALE, 0)
         gpu_ctx.set_option(rtow.RT_OPT_GRID_PHASE_X, 0)
         gpu_ctx.set_option(rtow.RT_OPT_GRID_PHASE_Z, 0)
+    for opt, bad in ((rtow.RT_OPT_GRID_PHASE_X, 1.0), (rtow.RT_OPT_GRID_PHASE_Z, -0.25)):
+        with pytest.raises(rtow.RTError):
+            gpu_ctx.set_option(opt, bad)
 
 
 @pytest.mark.parametrize("spp", [1000, 2000, 2047, 4096])
