@@ -7,7 +7,7 @@
 #include <cstdint>
 #include <vector>
 
-#include "rt.h"
+#include "rt_internal.h"
 #include "rt_layout.h"
 
 namespace rtk {
@@ -19,7 +19,7 @@ struct accel_options {
   double collapse = 0.35;    // RT_OPT_BVH_COLLAPSE
   double side = 1.0;         // RT_OPT_BVH_SIDE
   double grid_scale = 1.0;   // RT_OPT_GRID_SCALE
-  double grid_phase_x = 0.0, grid_phase_z = 0.0;  // RT_OPT_GRID_PHASE_X / _Z
+  double grid_phase_x = 0.0, grid_phase_z = 0.0;  // RT_OPT_INTERNAL_GRID_PHASE_X / _Z
   int grid_placement = -1;   // RT_OPT_GRID_PLACEMENT: -1 auto, else kGridGlobal / kGridLds / kGridCells
   bool wide = false;         // 64-bit pixel sums (an albedo above 1): less LDS for the grid
 };

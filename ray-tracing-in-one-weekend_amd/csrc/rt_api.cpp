@@ -14,10 +14,11 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <limits>
 #include <new>
 #include <vector>
 
-#include "rt.h"
+#include "rt_internal.h"
 #include "rt_accel.h"
 #include "rt_layout.h"
 
@@ -299,10 +300,10 @@ int rt_context_set_option(rt_context *c, int option, double v) {
       if (v != 0.0 && v != 1.0) return RT_ERR_INVALID;
       c->grid_fit = v != 0.0;
       return RT_OK;
-    case RT_OPT_GRID_PHASE_X:
-    case RT_OPT_GRID_PHASE_Z:
+    case RT_OPT_INTERNAL_GRID_PHASE_X:
+    case RT_OPT_INTERNAL_GRID_PHASE_Z:
       if (!(v >= 0.0 && v < 1.0)) return RT_ERR_INVALID;
-      (option == RT_OPT_GRID_PHASE_X ? c->opt.grid_phase_x : c->opt.grid_phase_z) = v;
+      (option == RT_OPT_INTERNAL_GRID_PHASE_X ? c->opt.grid_phase_x : c->opt.grid_phase_z) = v;
       return RT_OK;
     case RT_OPT_BVH_LEAF:
       if (v != std::floor(v) || v < 0 || v > 4) return RT_ERR_INVALID;
@@ -557,8 +558,8 @@ launch_plan plan_launches(const rt_params *prm, double launch_samples) {
   return launch_plan{units, ranges, chunks, entries};
 }
 
-int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, float *accum_rgb, hipStream_t st,
-                   hipEvent_t ev_start) {
+int render_enqueue_body(rt_context *c, const rt_camera *cam, const rt_params *prm, float *accum_rgb, hipStream_t st,
+                        hipEvent_t ev_start) {
   RT_HIP(hipSetDevice(c->device));
   // renders of one context are serialised, whatever streams they come on:
   // they share the block-order scratch buffer
@@ -599,18 +600,30 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
         c->fit_pending = false;
         rtk::grid_geom &q = c->fit_grid;
         if (!c->fitter->build(scale, q)) return RT_ERR_INVALID;  // (every candidate fits: unreachable)
+        // Transactional: larger buffers are allocated before the
+        // old ones are freed, so a failed allocation leaves the old grid whole
+        // (buffers, fields and fit_key describe it); once a copy into the
+        // buffers has failed they hold neither grid, and grid_scale = NaN makes
+        // the next grid render refit before it launches.
         if (q.cells.size() > c->cells_cap || q.items.size() / 4 > c->items_cap) {
-          RT_HIP(hipStreamSynchronize(st));
+          void *nc = nullptr, *ni = nullptr;
+          hipError_t ea = hipMalloc(&nc, q.cells.size() * sizeof(uint32_t));
+          if (ea == hipSuccess) ea = hipMalloc(&ni, q.items.size() * sizeof(float));
+          if (ea == hipSuccess) ea = hipStreamSynchronize(st);  // earlier renders on st still read the old grid
+          if (ea != hipSuccess) {
+            (void)hipFree(nc);
+            (void)hipFree(ni);
+            return hip_fail(ea);
+          }
           (void)hipFree(c->d_grid_cells);
           (void)hipFree(c->d_grid_items);
-          c->d_grid_cells = nullptr;
-          c->d_grid_items = nullptr;
-          c->cells_cap = c->items_cap = 0;
-          RT_HIP(hipMalloc(&c->d_grid_cells, q.cells.size() * sizeof(uint32_t)));
-          RT_HIP(hipMalloc(&c->d_grid_items, q.items.size() * sizeof(float)));
+          c->d_grid_cells = static_cast<uint32_t *>(nc);
+          c->d_grid_items = static_cast<float *>(ni);
           c->cells_cap = q.cells.size();
           c->items_cap = q.items.size() / 4;
         }
+        c->grid_scale = std::numeric_limits<double>::quiet_NaN();
+        c->fit_key.clear();
         RT_HIP(hipMemcpyAsync(c->d_grid_cells, q.cells.data(), q.cells.size() * sizeof(uint32_t),
                               hipMemcpyHostToDevice, st));
         RT_HIP(hipMemcpyAsync(c->d_grid_items, q.items.data(), q.items.size() * sizeof(float), hipMemcpyHostToDevice,
@@ -754,6 +767,21 @@ int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, fl
   c->last_stream = st;
   c->have_done = true;
   return RT_OK;
+}
+
+// A render that fails after enqueuing some of its work on st (a refit copy,
+// the pilot, the k-th launch) still ends with ev_done recorded on st, so that
+// the next render on another stream, and rt_scene_upload before it frees the
+// scene, wait for that work too (before, only hipFree's implicit
+// device synchronisation covered it).
+int render_enqueue(rt_context *c, const rt_camera *cam, const rt_params *prm, float *accum_rgb, hipStream_t st,
+                   hipEvent_t ev_start) {
+  const int r = render_enqueue_body(c, cam, prm, accum_rgb, st, ev_start);
+  if (r != RT_OK && c->ev_done && hipEventRecord(c->ev_done, st) == hipSuccess) {
+    c->last_stream = st;
+    c->have_done = true;
+  }
+  return r;
 }
 
 // rt_render's frame buffer (only it uses d_frame, and it returns after its

@@ -7,7 +7,7 @@
 // reference's argument lists, so the scene is the same whatever compiler
 // builds this file (hipcc/clang evaluates left-to-right and would otherwise
 // produce a different 484-sphere scene -- SURVEY 0.2 / 8a-1).
-#include "rt.h"
+#include "rt_internal.h"
 
 #include <algorithm>
 #include <cerrno>

@@ -37,7 +37,7 @@
 #include <type_traits>
 #include <utility>
 
-#include "rt.h"
+#include "rt_internal.h"
 #include "rt_layout.h"
 #include "rt_turn_table.h"
 

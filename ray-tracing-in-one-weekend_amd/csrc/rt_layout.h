@@ -15,7 +15,7 @@
 #include <cstddef>
 #include <cstdint>
 
-#include "rt.h"
+#include "rt_internal.h"
 
 namespace rtk {
 

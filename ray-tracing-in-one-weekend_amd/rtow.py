@@ -37,11 +37,11 @@ RT_FLAG_LAYER_BVH = 1 << 12  # layer scenes: walk the layer BVH instead of the l
 RT_CHUNK_SPP = 64  # include/rt.h: kept for compatibility (pixel sums are exact integers, units split evenly)
 RT_TONEMAP_CPU, RT_TONEMAP_GPU = 0, 1  # write_color of src/cpu (fp64) / src/gpu (fp32)
 RT_KAT_SPHERE_HIT, RT_KAT_REFLECT, RT_KAT_REFRACT, RT_KAT_REFLECTANCE = 0, 1, 2, 3
-ABI_VERSION = 5
+ABI_VERSION = 6
 # rt_context_set_option (include/rt.h): placement / shape / launch options, never semantics
 RT_OPT_GRID_PLACEMENT, RT_OPT_GRID_SCALE, RT_OPT_BVH_LEAF = 1, 2, 3
 RT_OPT_BVH_COLLAPSE, RT_OPT_BVH_SIDE, RT_OPT_LAUNCH_SAMPLES, RT_OPT_GRID_FIT = 4, 5, 6, 7
-RT_OPT_GRID_PHASE_X, RT_OPT_GRID_PHASE_Z = 8, 9
+RT_OPT_INTERNAL_GRID_PHASE_X, RT_OPT_INTERNAL_GRID_PHASE_Z = 8, 9  # include/rt_internal.h
 RT_GRID_AUTO, RT_GRID_LDS, RT_GRID_CELLS_LDS, RT_GRID_GLOBAL = 0, 1, 2, 3
 GRID_PLACEMENTS = {"auto": RT_GRID_AUTO, "lds": RT_GRID_LDS, "cells": RT_GRID_CELLS_LDS, "global": RT_GRID_GLOBAL}
 
@@ -342,8 +342,8 @@ class Context:
         if grid_scale is not None:
             self.set_option(RT_OPT_GRID_SCALE, grid_scale)
         if grid_phase is not None:
-            self.set_option(RT_OPT_GRID_PHASE_X, grid_phase[0])
-            self.set_option(RT_OPT_GRID_PHASE_Z, grid_phase[1])
+            self.set_option(RT_OPT_INTERNAL_GRID_PHASE_X, grid_phase[0])
+            self.set_option(RT_OPT_INTERNAL_GRID_PHASE_Z, grid_phase[1])
         v = scene.view()
         check(lib().rt_scene_upload(self._h, ctypes.byref(v)), "rt_scene_upload")
         self.scene = scene
@@ -431,7 +431,7 @@ def accel_info(scene, grid_mode="auto", grid_scale=0.0):
 def grid_fit(scene, cam, width, height, phase=(0.0, 0.0)):
     """What RT_OPT_GRID_FIT picks for `scene` seen by `cam` in a width x height
     frame, computed on the host (rt_internal_grid_fit_phase; no device), with
-    the grid origin shifted by `phase` cells (RT_OPT_GRID_PHASE_X / _Z): (cell
+    the grid origin shifted by `phase` cells (RT_OPT_INTERNAL_GRID_PHASE_X / _Z): (cell
     scale or 0.0 without an LDS grid, [(candidate scale, modelled cost)])."""
     L = lib()
     L.rt_internal_grid_fit_phase.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,

@@ -182,6 +182,53 @@ def test_async_renders_on_two_streams_are_ordered(rtow):
         assert np.array_equal(tb.cpu().numpy(), want_b)
 
 
+def test_grid_refit_between_async_renders_on_two_streams(rtow, oracle):
+    """RT_OPT_GRID_FIT (default on) refits the layer grid in place
+    inside render_enqueue, so a render with camera B overwrites the grid
+    buffers that camera A's render, still pending on another stream, reads.
+    Uploaded with defaults, A (fits 1.11) and B (fits 1.22) alternate on two
+    streams with no host sync between them: both images and segment counts
+    equal the oracle's, and after each render the context's cell scale is the
+    host model's pick for that geometry (rtow.grid_fit).  (The capacity-growth
+    branch of the refit is not reached: every candidate is at least as coarse
+    as the builder's grid, so it never needs larger buffers.)"""
+    import torch
+    scene = rtow.final_scene()
+    W, H = 320, 180
+    cam_a = rtow.camera_cpu(aspect=W / H)
+    cam_b = rtow.camera_cpu(lookfrom=(6, 1, 12), aspect=W / H)
+    fit_a, fit_b = rtow.grid_fit(scene, cam_a, W, H)[0], rtow.grid_fit(scene, cam_b, W, H)[0]
+    assert fit_a != fit_b, (fit_a, fit_b)  # precondition: B's render refits the grid
+    pa = rtow.make_params(W, H, 24, seed=31, flags=GRID, units=2)
+    pb = rtow.make_params(W, H, 24, seed=32, flags=GRID, units=2)
+    want_a, segs_a = kernel_render(scene, cam_a, pa)
+    want_b, segs_b = kernel_render(scene, cam_b, pb)
+    with rtow.Context(0) as ctx:
+        ctx.upload(scene)
+        dev = torch.device("cuda", 0)
+        s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        ta = torch.zeros((H, W, 3), dtype=torch.float32, device=dev)
+        tb = torch.zeros_like(ta)
+        torch.cuda.synchronize(dev)
+        ctx.render_async(cam_a, pa, ta.data_ptr(), s1.cuda_stream)
+        assert ctx.grid_scale() == pytest.approx(fit_a, abs=1e-12)
+        ctx.render_async(cam_b, pb, tb.data_ptr(), s2.cuda_stream)  # refits while A may be pending
+        assert ctx.grid_scale() == pytest.approx(fit_b, abs=1e-12)
+        torch.cuda.synchronize(dev)
+        st_b = ctx.collect_stats()
+        assert np.array_equal(ta.cpu().numpy(), want_a)
+        assert np.array_equal(tb.cpu().numpy(), want_b)
+        assert st_b.segments == segs_b
+        # and back to A on the second stream, then B on the first
+        for cam, p, t, s, fit, want, segs in ((cam_a, pa, tb, s2, fit_a, want_a, segs_a),
+                                              (cam_b, pb, ta, s1, fit_b, want_b, segs_b)):
+            ctx.render_async(cam, p, t.data_ptr(), s.cuda_stream)
+            assert ctx.grid_scale() == pytest.approx(fit, abs=1e-12)
+            torch.cuda.synchronize(dev)
+            assert np.array_equal(t.cpu().numpy(), want)
+            assert ctx.collect_stats().segments == segs
+
+
 def test_pilot_first_render_is_asynchronous_and_correct(rtow):
     """The pilot schedule's first render of a geometry enqueues the pilot, the
     device sort and the render without a host sync; the result equals launch
@@ -305,7 +352,7 @@ def test_grid_cell_scales_render_the_oracle_image(rtow, gpu_ctx, oracle, half_ex
     """The layer grid's cell size (RT_OPT_GRID_SCALE) is scheduling only: the
     headline scene (grid in LDS) and C4's (cells in LDS) uploaded at the
     builder's scale s0 and at s0 (1 + 0.01 k), k = 3, 7, 15, 30, and with the
-    grid's origin shifted by a fraction of a cell (RT_OPT_GRID_PHASE_X / _Z),
+    grid's origin shifted by a fraction of a cell (RT_OPT_INTERNAL_GRID_PHASE_X / _Z),
     render the oracle's image bit for bit with equal segments (the lists hold
     every sphere that can win)."""
     scene = rtow.final_scene(half_extent=half_extent)
@@ -323,9 +370,9 @@ def test_grid_cell_scales_render_the_oracle_image(rtow, gpu_ctx, oracle, half_ex
             assert st.segments == segs, (k, ph)
     finally:
         gpu_ctx.set_option(rtow.RT_OPT_GRID_SCALE, 0)
-        gpu_ctx.set_option(rtow.RT_OPT_GRID_PHASE_X, 0)
-        gpu_ctx.set_option(rtow.RT_OPT_GRID_PHASE_Z, 0)
-    for opt, bad in ((rtow.RT_OPT_GRID_PHASE_X, 1.0), (rtow.RT_OPT_GRID_PHASE_Z, -0.25)):
+        gpu_ctx.set_option(rtow.RT_OPT_INTERNAL_GRID_PHASE_X, 0)
+        gpu_ctx.set_option(rtow.RT_OPT_INTERNAL_GRID_PHASE_Z, 0)
+    for opt, bad in ((rtow.RT_OPT_INTERNAL_GRID_PHASE_X, 1.0), (rtow.RT_OPT_INTERNAL_GRID_PHASE_Z, -0.25)):
         with pytest.raises(rtow.RTError):
             gpu_ctx.set_option(opt, bad)
 

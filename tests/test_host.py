@@ -201,9 +201,16 @@ def test_ppm_writer_p3_and_p6(rtow, tmp_path):
 
 
 def test_abi_exports_every_declared_symbol(rtow):
-    hdr = open(os.path.join(ROOT, "include", "rt.h")).read()
-    names = sorted(set(re.findall(r"^\s*(?:[\w\*\s]+?)\b(rt_\w+)\s*\(", hdr, re.M)))
-    assert len(names) == 28, names
+    """Every function include/rt.h (the drop-in boundary) and include/
+    rt_internal.h (tests' and tools' diagnostics) declare is
+    exported; the public header declares no diagnostic."""
+    decl = r"^\s*(?:[\w\*\s]+?)\b(rt_\w+)\s*\("
+    pub = sorted(set(re.findall(decl, open(os.path.join(ROOT, "include", "rt.h")).read(), re.M)))
+    internal = sorted(set(re.findall(decl, open(os.path.join(ROOT, "include", "rt_internal.h")).read(), re.M)))
+    assert len(pub) == 21 and len(internal) == 7, (pub, internal)
+    assert not [n for n in pub if n.startswith("rt_internal_") or n == "rt_device_kat"], pub
+    assert "RT_OPT_GRID_PHASE" not in open(os.path.join(ROOT, "include", "rt.h")).read()
+    names = pub + internal
     L = rtow.lib()
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
@@ -263,7 +270,7 @@ def test_invalid_arguments_return_status(rtow):
     assert L.rt_scene_final(11, None, None) == -1
     assert L.rt_tonemap_u8(None, 4, 10, None) == -1
     assert L.rt_strerror(-4) == b"no such HIP device"
-    assert L.rt_abi_version() == rtow.ABI_VERSION == 5
+    assert L.rt_abi_version() == rtow.ABI_VERSION == 6
     with pytest.raises(rtow.RTError):
         rtow.camera_cpu(aspect=0.0)
 
@@ -353,7 +360,7 @@ def test_grid_fit_picks_a_candidate_per_camera(rtow):
 
 
 def test_grid_phase_keeps_the_grid_invariants(rtow):
-    """RT_OPT_GRID_PHASE_X / _Z (the grid's origin shifted by a fraction of a
+    """RT_OPT_INTERNAL_GRID_PHASE_X / _Z (the grid's origin shifted by a fraction of a
     cell): the fitter's candidates at every phase are grids the
     placement holds, the model's costs differ with the phase (the cell borders
     move relative to the spheres) and phases outside [0, 1) are refused."""

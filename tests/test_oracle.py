@@ -557,11 +557,12 @@ def test_tmin_in_ray_parameter_units_contact_fixture(rtow):
     reference's segment counts from 8 independent streams (tests/golden/
     make_contact_noise_golden.py; per-render spread 9e-5), with the
     opaque-inside rule off (it only shortens paths the reference traces to
-    the depth cap, black either way): the specification matches the
-    reference (8 seeds: -2e-5, 0.5 sigma); the round-4 t_min unit (0.001
-    world units on the normalised ray) loses 1.8e-4 of the segments
-    (paired); without the same-sphere exit rule the kernel traces 4.7e-4 too
-    many (fake entries into balls it starts on)."""
+    the depth cap, black either way): over the 4 seeds this test runs, the
+    specification matches the reference (-3.7e-5, -0.8 sigma; DESIGN.md 4's
+    8-seed run: -2.2e-5, -0.5 sigma); the round-4 t_min unit (0.001 world
+    units on the normalised ray) loses 1.83e-4 of the segments (paired);
+    without the same-sphere exit rule the kernel traces 4.5e-4 too many (fake
+    entries into balls it starts on; 4.7e-4 over 8 seeds)."""
     import json
     import fixture_scenes
     from oracle_lib import RTO_OPT_NO_SAME_EXIT, RTO_OPT_NO_SEALED, RTO_OPT_TMIN_WORLD, _kernel_render_opts

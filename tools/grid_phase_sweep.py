@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""The layer grid's origin phase (RT_OPT_GRID_PHASE_X / _Z) against the walk's
+"""The layer grid's origin phase (RT_OPT_INTERNAL_GRID_PHASE_X / _Z) against the walk's
 time (GPU box).  For one frame geometry (a bench preset, optionally one rank's
 share) and one cell scale (default: the fitter's pick), renders the grid with
 its origin shifted by (i / P, j / P) cells, i, j = 0..P-1, each `--reps` times

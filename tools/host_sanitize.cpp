@@ -12,7 +12,7 @@
 #include <unistd.h>
 #include <vector>
 
-#include "rt.h"
+#include "rt_internal.h"
 
 #define CHECK(x)                                                    \
   do {                                                              \
