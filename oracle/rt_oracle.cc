@@ -400,6 +400,7 @@ struct kctx {
   bool no_sealed = false;   // without the opaque-inside rule (RTO_OPT_NO_SEALED, attribution only)
   bool fp64_roots = false;  // candidates' roots in fp64 (RTO_OPT_FP64_ROOTS, attribution only)
   bool same_exit = true;    // the same-sphere exit rule (RTO_OPT_NO_SAME_EXIT turns it off)
+  bool fp64_hit = false;    // the winner's root, hit point and normal in fp64 (RTO_OPT_FP64_HIT, attribution only)
 };
 
 // the sum format's dither draw (rt_kernel.hip dither_u): pcg4d keyed by the
@@ -631,6 +632,30 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
       nn[2] = (p[2] - sc.cz[b]) * sc.inv_r[b];
       // front face from the root taken (exact-arithmetic equivalent of
       // dot(d, outward) < 0, hittable.h:16-19; outward flips for r < 0)
+      if (k.fp64_hit) {
+        // attribution only (RTO_OPT_FP64_HIT): the winner's root from the
+        // fp64 quadratic on the fp32 ray and sphere (the reference's
+        // sphere::hit arithmetic, sphere.h:24-51, |d| = 1 here), and the hit
+        // point and normal from it in fp64, rounded once to fp32
+        const double c3[3] = {sc.cx[b], sc.cy[b], sc.cz[b]}, rr = sc.radius[b];
+        double oc[3], hb = 0.0, cq = -rr * rr, dd = 0.0;
+        for (int a = 0; a < 3; ++a) {
+          oc[a] = (double)o[a] - c3[a];
+          hb += oc[a] * (double)d[a];
+          cq += oc[a] * oc[a];
+          dd += (double)d[a] * (double)d[a];
+        }
+        const double disc = hb * hb - dd * cq;
+        if (disc >= 0.0) {
+          const double sq = std::sqrt(disc);
+          const double td = (near ? (-hb - sq) : (-hb + sq)) / dd;
+          for (int a = 0; a < 3; ++a) {
+            const double pd = (double)o[a] + td * (double)d[a];
+            p[a] = (float)pd;
+            nn[a] = (float)((pd - c3[a]) / rr);
+          }
+        }
+      }
       const bool front = near != (sc.inv_r[b] < 0.0f);
       if (!front)
         for (int a = 0; a < 3; ++a) nn[a] = -nn[a];
@@ -1214,6 +1239,7 @@ int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, co
   k.no_sealed = (opts & RTO_OPT_NO_SEALED) != 0;
   k.fp64_roots = (opts & RTO_OPT_FP64_ROOTS) != 0;
   k.same_exit = (opts & RTO_OPT_NO_SAME_EXIT) == 0;
+  k.fp64_hit = (opts & RTO_OPT_FP64_HIT) != 0;
   if (exact) std::memset(exact, 0, 3 * sizeof(double) * (size_t)p->local_rows * (size_t)p->width);
   if (threads < 1) {
     // the machine's cores, but no more than OMP_NUM_THREADS (16 on the GPU

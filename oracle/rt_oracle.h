@@ -55,9 +55,13 @@ int rto_kernel_render(const rt_scene_view *scene, const rt_camera *cam, const rt
  *                      (attribution only: is the fp32 root the cause?);
  *   RTO_OPT_NO_SAME_EXIT without round 5's same-sphere exit rule (the exiting
  *                      root of the sphere a ray starts on, moving away from
- *                      its centre, taken as a hit: the round-4 form). */
+ *                      its centre, taken as a hit: the round-4 form);
+ *   RTO_OPT_FP64_HIT   the winning sphere's root, hit point and normal from
+ *                      fp64 arithmetic on the fp32 ray and sphere, rounded
+ *                      once (attribution only: is the fp32 hit point the
+ *                      cause?). */
 enum { RTO_OPT_NO_DITHER = 1, RTO_OPT_TMIN_WORLD = 2, RTO_OPT_NO_SEALED = 4, RTO_OPT_FP64_ROOTS = 8,
-       RTO_OPT_NO_SAME_EXIT = 16 };
+       RTO_OPT_NO_SAME_EXIT = 16, RTO_OPT_FP64_HIT = 32 };
 int rto_kernel_render_exact(const rt_scene_view *scene, const rt_camera *cam, const rt_params *p,
                             float *out, double *exact, int opts, unsigned long long *segments,
                             int threads);

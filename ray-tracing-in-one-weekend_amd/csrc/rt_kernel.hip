@@ -50,6 +50,36 @@ namespace rtk {
 #define RT_COUNT_ITEMS 0
 #endif
 
+// RT_LANE_PROFILE builds (tools/lane_profile.py, a measurement variant built
+// by tools/build_variant.sh; never the product): per source region of the
+// bounce loop, how many times a wave ran it, the lanes active (exec) and the
+// lanes that needed it (`useful`), counted in LDS by the wave's first active
+// lane and added to g_lane_prof at the wave's end (DESIGN.md 8's lane table).
+// The default build compiles every LP() to nothing.
+enum {
+  kLpStep = 0, kLpClosest, kLpExtrasLead, kLpExtrasRound, kLpGridWalk, kLpDda, kLpItem, kLpGridCand,
+  kLpSky, kLpHit, kLpLamb, kLpMetal, kLpDiel, kLpCamera, kLpSkip, kLpTail, kLpRegions
+};
+#ifdef RT_LANE_PROFILE
+__device__ unsigned long long g_lane_prof[kLpRegions * 3];
+__shared__ uint32_t s_lane_prof[4][kLpRegions][3];
+__device__ __forceinline__ void lane_prof(int r, bool useful) {
+  const uint64_t m = __builtin_amdgcn_ballot_w64(true);
+  const uint64_t u = __builtin_amdgcn_ballot_w64(useful);
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  if (l == __builtin_ctzll(m)) {
+    uint32_t *c = s_lane_prof[__builtin_amdgcn_readfirstlane((int)threadIdx.x) >> 6][r];
+    c[0] += 1u;
+    c[1] += (uint32_t)__builtin_popcountll(m);
+    c[2] += (uint32_t)__builtin_popcountll(u);
+  }
+}
+#define LP(r, useful) lane_prof((r), (useful))
+#else
+#define LP(r, useful) ((void)0)
+#endif
+
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 // the dynamic LDS of the LDS grid placements: kGridLds the grid items, then
@@ -449,6 +479,7 @@ __device__ __forceinline__ void scan_extras(const RT_CONST pair_geom *__restrict
   constexpr int J0 = LEAD ? 1 : 0;
   if (LEAD) {
     if (__builtin_amdgcn_ballot_w64(c[0])) {  // a wave-uniform branch
+      LP(kLpExtrasLead, c[0]);
       if (STATS) ++roots;
       candidate<OPEN>(c[0], h[0], d[0], t[0], tmin, hs);
     }
@@ -474,6 +505,7 @@ __device__ __forceinline__ void scan_extras(const RT_CONST pair_geom *__restrict
       taken = taken || f;
     }
     if (!__builtin_amdgcn_ballot_w64(taken)) break;
+    LP(kLpExtrasRound, taken);
     if (STATS) ++roots;
     candidate<OPEN>(taken, hh, dd, tt, tmin, hs);
   }
@@ -584,8 +616,12 @@ __device__ __forceinline__ void grid_item(const f4 it, float dx, float dz, const
   // it.w holds tie2_of<false>(index); the open interval's is 0xfffffffe - it
   const uint32_t w = __float_as_uint(it.w);
   const bool c = e >= it.z;
+  LP(kLpItem, true);
   // a wave-uniform branch; the sequence runs under the item loop's own mask
-  if (__builtin_amdgcn_ballot_w64(c)) candidate<OPEN>(c, h, e - it.z, OPEN ? 0xfffffffeu - w : w, tmin, hs);
+  if (__builtin_amdgcn_ballot_w64(c)) {
+    LP(kLpGridCand, c);
+    candidate<OPEN>(c, h, e - it.z, OPEN ? 0xfffffffeu - w : w, tmin, hs);
+  }
   if (STATS) ++wc.tests;
 }
 
@@ -610,6 +646,7 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
   const float az = fmaf(p.grid_zi, iz, oiz), bz = fmaf(p.grid_z1, iz, oiz);
   ta = fmaxf(ta, fmaxf(fminf(ax, bx), fminf(az, bz)));
   tb = fminf(tb, fminf(fmaxf(ax, bx), fmaxf(az, bz)));
+  LP(kLpGridWalk, ta <= tb);
   if (!(ta <= tb)) return;
   const float dx = rl.dx.x, dz = rl.dz.x;
   const float px = fmaf(ta, dx, ox), pz = fmaf(ta, dz, oz);
@@ -638,6 +675,7 @@ __device__ __forceinline__ void grid_walk(float ox, float oz, float ix, float iz
   const int dcx = (nxs ? -1 : 1) * (LC ? 2 : 1), dcz = (nzs ? -nx : nx) * (LC ? 2 : 1);
   typedef const __attribute__((address_space(3))) uint16_t lds_u16;
   while (true) {
+    LP(kLpDda, true);
     // STATS: boxes = lane-level cell visits; box_hits / roots = wave-level DDA
     // / item iterations (counted once per wave, by its first active lane)
     if (STATS) {
@@ -713,6 +751,7 @@ __device__ __forceinline__ hit_state closest_hit(float ox, float oy, float oz, f
   const RT_CONST bvh_node *__restrict__ nodes = as_const(p.nodes);
   const RT_CONST int *__restrict__ orig = as_const(p.orig);
   const int n_pairs = p.n_pad / 2;
+  LP(kLpClosest, true);
   const float nk1 = -dot3(ox, oy, oz, dx, dy, dz);
   const float o2 = dot3(ox, oy, oz, ox, oy, oz);
   const float ox2 = -2.0f * ox, oy2 = -2.0f * oy, oz2 = -2.0f * oz;
@@ -887,6 +926,9 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
     }
   }
   s_sum[0][threadIdx.x] = s_sum[1][threadIdx.x] = s_sum[2][threadIdx.x] = 0u;
+#ifdef RT_LANE_PROFILE
+  if ((threadIdx.x & 63) < kLpRegions * 3) (&s_lane_prof[threadIdx.x >> 6][0][0])[threadIdx.x & 63] = 0u;
+#endif
   if (GP == kGridLds) {  // the block's copy of the layer grid (kparams grid_n_items)
     const RT_GLOBAL f4 *gi = as_global(p.grid_items);
     for (int i = (int)threadIdx.x; i < p.grid_n_items; i += kBlock) s_grid_dyn[i] = gi[i];
@@ -950,6 +992,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
   // for it (the step body then runs under the alive lanes' mask, with no
   // wave-level any-alive ballot per step)
   while (alive) {
+    LP(kLpStep, tracing);
     hit_state hs = no_hit();
     if (tracing) hs = closest_hit<OPEN, BVH, STATS, GRID, GP>(ox, oy, oz, dx, dy, dz, tmin, wc);
     ++steps;
@@ -969,6 +1012,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
       const kparams q = kernargs();  // shading's parameters, re-read per step
       if (tracing) ++segs;
       if (tracing && best < 0) {
+        LP(kLpSky, true);
         // miss: sky gradient, src/cpu/main.cc:27-29; the sample's radiance
         // goes into its pixel's fixed-point sum
         const float a = 0.5f * (dy + 1.0f);
@@ -1012,6 +1056,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
       polar(miss ? unif(r.z) : fmaf(-uz, uz, 1.0f), unif(miss ? r.w : r.y), ux, uy);
 
       if (!miss) {
+        LP(kLpHit, true);
         const float o2 = dot3(ox, oy, oz, ox, oy, oz);
         const float ox2 = -2.0f * ox, oy2 = -2.0f * oy, oz2 = -2.0f * oz;
         const float tmax = hs.tmax;
@@ -1045,6 +1090,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           } else {
             tmin = __uint_as_float(__float_as_uint(tmax) + 1u);  // nextafter(tmax, +inf), tmax > 0 finite
           }
+          LP(kLpSkip, true);
           skipped = true;
           --segs;
         } else {
@@ -1069,6 +1115,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         bool scattered = true;
         const uint32_t kind = sr.kind;
         if (kind == RT_LAMBERTIAN) {
+          LP(kLpLamb, true);
           // The opaque-inside rule: a sealed lambertian
           // sphere (no other ball overlaps its ball, rt_accel.cpp
           // sealed_spheres) hit at its exiting root -- the ray started inside
@@ -1093,6 +1140,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           }
         }
         if (kind == RT_METAL) {
+          LP(kLpMetal, true);
           // material.h:40-46
           float fz = sr.param;
           if (!METAL_UNIT) fz *= ball_radius(r);  // random_in_unit_sphere
@@ -1102,6 +1150,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
           scattered = dot3(sx, sy, sz, nx, ny, nz) > 0.0f;
         }
         if (kind >= RT_DIELECTRIC) {
+          LP(kLpDiel, true);
           // dielectric, material.h:57-87 (r0 is the same for ior and 1/ior)
           const float ratio = front ? sr.inv_param : sr.param;
           const float cos_t = fminf(-dn, 1.0f);
@@ -1133,6 +1182,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         }
         }
       } else if (tracing) {
+        LP(kLpCamera, true);
         // a new item: its camera ray, with the lens sample drawn above
         int col, grow;
         pixel_cr(q, col, grow);
@@ -1146,6 +1196,7 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
     // step: the lane takes its next item with the misses of the next step
     // (one camera-ray path per step, with the step's one hash)
     if (path_done) tracing = false;
+    LP(kLpTail, true);
     // one normalize3 per lane and step: the bounce direction or the new
     // camera ray's (a finished lane's is unused), and with it the ray's t_min
     // (a skipped ray keeps its own)
@@ -1166,13 +1217,19 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
         out[1] = (float)s_sum[1][i] * q.qinv;
         out[2] = (float)s_sum[2][i] * q.qinv;
       } else {  // the tile's units / launches add their integer sums (finish_sums converts)
-        sum_t *acc = reinterpret_cast<sum_t *>(q.out) + o;  // WIDE: the context's 64-bit scratch frame
-        atomicAdd(acc + 0, s_sum[0][i]);
-        atomicAdd(acc + 1, s_sum[1][i]);
-        atomicAdd(acc + 2, s_sum[2][i]);
+        // (global, not generic, atomics: the product's device code holds no
+        // flat memory instruction, DESIGN.md 8 "the v7 fault")
+        RT_GLOBAL sum_t *acc = reinterpret_cast<RT_GLOBAL sum_t *>(as_global(q.out)) + o;  // WIDE: the 64-bit scratch frame
+        __hip_atomic_fetch_add(acc + 0, s_sum[0][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(acc + 1, s_sum[1][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(acc + 2, s_sum[2][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
+#ifdef RT_LANE_PROFILE
+  if (lane < kLpRegions * 3)
+    atomicAdd(&g_lane_prof[lane], (unsigned long long)(&s_lane_prof[wave][0][0])[lane]);
+#endif
   // one atomic per wave for the counters
   uint32_t s = segs;
   // wave-steps: the most any lane of the wave looped
@@ -1195,18 +1252,21 @@ __global__ __launch_bounds__(kBlock, 8) void render_kernel(const kparams p) {
       if (k.tile_cost) {
         // and nothing else: 6 same-address atomics from each of ~10^5 short
         // waves serialise (the 4-spp pilot took 9.5 ms instead of ~1.2)
-        k.tile_cost[(int)blockIdx.x * kWavesPerBlock + wave] = s;
+        as_global(k.tile_cost)[(int)blockIdx.x * kWavesPerBlock + wave] = s;
         return;
       }
     }
-    unsigned long long *counters = kernargs().counters + 8 * (blockIdx.x & (kCounterSlots - 1));
-    atomicAdd(&counters[0], (unsigned long long)s);
-    atomicAdd(&counters[1], (unsigned long long)ws);
+    RT_GLOBAL unsigned long long *counters = as_global(kernargs().counters) + 8 * (blockIdx.x & (kCounterSlots - 1));
+    auto add = [](RT_GLOBAL unsigned long long *a, unsigned long long v) {
+      __hip_atomic_fetch_add(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    add(&counters[0], s);
+    add(&counters[1], ws);
     if (STATS) {
-      atomicAdd(&counters[2], (unsigned long long)lt);
-      atomicAdd(&counters[3], (unsigned long long)lb);
-      atomicAdd(&counters[4], (unsigned long long)lh);
-      atomicAdd(&counters[5], (unsigned long long)lr);
+      add(&counters[2], lt);
+      add(&counters[3], lb);
+      add(&counters[4], lh);
+      add(&counters[5], lr);
     }
   }
 }
@@ -1406,3 +1466,16 @@ hipError_t upload_turn_table() {
 }
 
 }  // namespace rtk
+
+#ifdef RT_LANE_PROFILE
+// the measurement variant's counters (tools/lane_profile.py): read (and, with
+// reset != 0, zero) the kLpRegions x (waves, exec lanes, useful lanes) sums
+extern "C" int rt_lane_profile_read(unsigned long long *out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rtk::g_lane_prof), sizeof(rtk::g_lane_prof)) != hipSuccess) return -2;
+  if (reset) {
+    static const unsigned long long zero[rtk::kLpRegions * 3] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rtk::g_lane_prof), zero, sizeof(zero)) != hipSuccess) return -2;
+  }
+  return rtk::kLpRegions;
+}
+#endif

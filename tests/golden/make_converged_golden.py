@@ -59,7 +59,10 @@ def main():
         scene, k = job
         r = subprocess.run([HARNESS, "render", str(W), str(ASPN), str(ASPD), str(a.spp), str(DEPTH),
                             arg[scene], str(k * SKIP_STRIDE)], check=True, capture_output=True)
-        with gzip.open(os.path.join(HERE, name(scene, a.spp, k)), "wb", mtime=0) as f:
+        with open(os.path.join(tempfile.gettempdir(), name(scene, a.spp, k)[:-3]), "wb") as f:
+            f.write(r.stdout)  # (a raw copy first: a long render is not lost to a write error)
+        with open(os.path.join(HERE, name(scene, a.spp, k)), "wb") as raw, \
+                gzip.GzipFile(fileobj=raw, mode="wb", mtime=0) as f:
             f.write(r.stdout)
         st = json.loads(r.stderr.decode().strip().splitlines()[-1])
         print(scene, k, st, flush=True)

@@ -3,7 +3,7 @@
 the REFERENCE itself (oracle/_ref/ref_harness, built from /root/reference's
 src/cpu) rendering each of tests/random_scenes.py's 24 scenes at the test's
 96x54x64, depth 50, with the final scene's camera, from 6 independent
-streams (SKIP = k * 10^7 draws after the scene) -> the image-mean of every
+streams (SKIP = k * 10^7 draws after the scene; one stream draws ~5*10^6; 6 streams until round 5, 24 since round 6) -> the image-mean of every
 stream per channel, in tests/golden/ref_random_scenes_means.json.  The
 stream-to-stream spread of those means is the reference's own noise on each
 scene, against which tests/test_oracle.py bounds the kernel algorithm's bias.
@@ -21,7 +21,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
-W, SPP, DEPTH, STREAMS = 96, 64, 50, 6
+W, SPP, DEPTH, STREAMS = 96, 64, 50, 24
 
 
 def main():
@@ -50,7 +50,7 @@ def main():
         return k, j, img.mean(0).tolist(), seg
 
     out = {}
-    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+    with ThreadPoolExecutor(max_workers=int(os.environ.get("JOBS", min(8, os.cpu_count() or 1)))) as ex:
         for k, j, mean, seg in ex.map(one, jobs):
             e = out.setdefault(str(k), {"width": W, "spp": SPP, "depth": DEPTH, "means": [None] * STREAMS,
                                         "segments": [None] * STREAMS})

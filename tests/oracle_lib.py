@@ -76,6 +76,7 @@ RTO_OPT_TMIN_WORLD = 2
 RTO_OPT_NO_SEALED = 4
 RTO_OPT_FP64_ROOTS = 8
 RTO_OPT_NO_SAME_EXIT = 16
+RTO_OPT_FP64_HIT = 32
 
 
 def kernel_render(scene, cam, params, threads=0, tmin_world=False, no_sealed=False):

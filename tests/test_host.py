@@ -535,3 +535,32 @@ def test_sealed_touching_and_tiny_spheres(rtow, oracle):
     assert rtow.sealed(overlap).tolist() == [False, False]
     for s in (touching, apart, overlap):
         assert np.array_equal(rtow.sealed(s), oracle.sealed(s))
+
+
+def test_device_code_has_no_flat_memory_instructions(rtow, tmp_path):
+    """No generic-pointer (flat) load, store or atomic anywhere in librtow.so's
+    gfx950 code ("the v7 fault"): the walk reads LDS through
+    address_space(3) pointers (ds_*) and the grid, records and frame through
+    address_space(1) ones (global_*), so no address is ever formed from an
+    LDS offset plus the shared aperture.  Round 5's unshipped v7 variant read
+    its hot items through flat loads and faulted with
+    HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION (profiles/r05p_v7tests_fault.log),
+    the code of a flat address outside every aperture and outside the
+    canonical range: an LDS-aperture pointer with a negative offset.  Since
+    round 6 the epilogue's atomics are global too, so a flat instruction
+    appearing here is a regression to look at."""
+    import shutil
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not (os.path.exists(os.path.join(llvm, "llvm-objdump")) and shutil.which("objcopy")):
+        pytest.skip("llvm-objdump / objcopy not available")
+    fat = tmp_path / "fatbin.bin"
+    co = tmp_path / "gfx950.co"
+    subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", rtow.LIB_PATH, str(fat)], check=True)
+    subprocess.run([os.path.join(llvm, "clang-offload-bundler"), "--unbundle", "--type=o", "--input=" + str(fat),
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + str(co)], check=True)
+    dis = subprocess.run([os.path.join(llvm, "llvm-objdump"), "-d", "--no-show-raw-insn", str(co)],
+                         check=True, capture_output=True, text=True).stdout
+    ops = re.findall(r"^\s+((?:flat|global|ds)_\w+)", dis, re.M)
+    assert sum(o.startswith("global_") for o in ops) > 100 and sum(o.startswith("ds_") for o in ops) > 100
+    flat = sorted(set(o for o in ops if o.startswith("flat_")))
+    assert not flat, flat
