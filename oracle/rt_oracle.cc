@@ -126,6 +126,8 @@ bool sphere_hit(const dsphere &s, d3 o, d3 d, double tmin, double tmax, dhit &re
 }
 
 unsigned long long g_last_trapped = 0;  // rto_reference_trapped
+unsigned long long g_last_capped = 0;   // rto_reference_capped
+std::atomic<unsigned long long> g_kcapped{0};  // rto_kernel_capped
 // kernel mode, attribution only (rto_kernel_attrib): spurious-root skips,
 // first hits on the inside of a sealed sphere, and those of them whose ray
 // had just been moved on by a skip
@@ -142,6 +144,7 @@ struct dworld {
   // reference traces after a path's first hit on the inside of one
   std::vector<uint8_t> sealed;
   unsigned long long trapped = 0;
+  unsigned long long capped = 0;  // paths ended at the depth cap (rto_reference_capped)
   // hittable_list.h:28-43
   bool hit(d3 o, d3 d, double tmin, double tmax, dhit &rec) {
     ++calls;
@@ -208,7 +211,10 @@ bool scatter(const dsphere &m, d3 din, const dhit &rec, rng64 &r, d3 &att, d3 &d
 // main.cc:12-30 (recursive); trapped: the path has hit a sealed sphere from
 // inside (counted in w.trapped, nothing else changes)
 d3 ray_color(d3 o, d3 d, dworld &w, rng64 &r, int depth, bool trapped = false) {
-  if (depth <= 0) return {0, 0, 0};
+  if (depth <= 0) {
+    ++w.capped;
+    return {0, 0, 0};
+  }
   dhit rec;
   if (trapped) ++w.trapped;
   if (w.hit(o, d, 0.001, INFINITY, rec)) {
@@ -724,6 +730,7 @@ unsigned long long kernel_pixel(const kctx &k, int col, int grow, float acc[3]) 
       if (wide)  // albedos above 1: the throughput stays finite (the kernel's clamp)
         for (int a = 0; a < 3; ++a) th[a] = std::fmin(th[a], 0x1p100f);
       ++depth;
+      if (scattered && depth >= k.p->max_depth) g_kcapped.fetch_add(1, std::memory_order_relaxed);
       if (!scattered || depth >= k.p->max_depth) break;
       for (int a = 0; a < 3; ++a) {
         o[a] = p[a];
@@ -1203,11 +1210,18 @@ int reference_render_world(dworld &w, rng64 &r, d3 lookfrom, d3 lookat, double a
   }
   if (segments) *segments = w.calls;
   g_last_trapped = w.trapped;
+  g_last_capped = w.capped;
   return 0;
 }
 }  // namespace
 
 unsigned long long rto_reference_trapped() { return g_last_trapped; }
+unsigned long long rto_reference_capped() { return g_last_capped; }
+unsigned long long rto_kernel_capped(int reset) {
+  const unsigned long long v = g_kcapped.load();
+  if (reset) g_kcapped = 0;
+  return v;
+}
 
 void rto_kernel_attrib(unsigned long long *out, int reset) {
   out[0] = g_skips.load();

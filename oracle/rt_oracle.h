@@ -17,6 +17,11 @@ extern "C" {
  * opaque-inside rule's spheres), which the kernel's rule
  * does not trace. */
 unsigned long long rto_reference_trapped(void);
+/* Attribution only: paths the last rto_reference_render(_view) ended at the
+ * depth cap (ray_color's depth <= 0, src/cpu/main.cc:16-17), and kernel-mode
+ * paths ended there since the last reset (reset != 0 zeroes it). */
+unsigned long long rto_reference_capped(void);
+unsigned long long rto_kernel_capped(int reset);
 /* Attribution only: kernel-mode counters summed over every render since the
  * last reset: out[0] spurious-root skips, out[1] paths' first hits on the
  * inside of a sealed sphere, out[2] those whose ray had just been moved on by

@@ -34,6 +34,26 @@ def free_scene(rtow, seed):
                       kind.astype(np.uint32), albedo.astype(f32), param.astype(f32))
 
 
+def ground_cut_spheres(scene):
+    """Indices of the spheres whose surface crosses the r = 1000 ground's
+    (fp64: 1000 - |r| < |C - G| < 1000 + |r|), [] without the ground.  Such a
+    sphere and the ground enclose a cavity (inside the ball, above the
+    ground) that the reference's paths enter through the crease more often
+    than the fp32 kernel algorithm's ("ground-cut spheres")."""
+    g = [i for i in range(scene.n) if float(scene.radius[i]) == 1000.0 and float(scene.cy[i]) == -1000.0]
+    if not g:
+        return []
+    out = []
+    for i in range(scene.n):
+        if i == g[0]:
+            continue
+        d = np.sqrt(float(scene.cx[i]) ** 2 + (float(scene.cy[i]) + 1000.0) ** 2 + float(scene.cz[i]) ** 2)
+        r = abs(float(scene.radius[i]))
+        if 1000.0 - r < d < 1000.0 + r:
+            out.append(i)
+    return out
+
+
 def dump_scene_exact(scene, path):
     """The scene in ref_harness's `file:` format, each float32 value printed
     as its exact double (%.17g), so the reference reads the same doubles the

@@ -72,45 +72,108 @@ def test_kernel_algorithm_matches_reference_random_scenes(rtow):
     """The fp32 kernel algorithm against the reference on the 24 random scenes
     at 96x54x64 (tests/random_scenes.py: overlapping and nested spheres,
     negative-radius glass shells, metal fuzz above 1, indices of refraction
-    below 1, spheres sunk into the ground), against the reference's own noise:
-    its image means from 6 independent streams (tests/golden/
-    make_random_noise_golden.py runs oracle/_ref/ref_harness, the reference's
-    src/cpu) and 8 seeds of the kernel algorithm.  Every channel's bias is
-    within 0.1 level (a tenth of north_star's 1/255) and within 5 sigma of
-    the two noises; segments within 1 %.  Measured (round 5):
-    worst bias 0.064 level; 69 of 72 channels within 2.5 sigma, the other
-    three (3.0-4.1 sigma, 0.04-0.06 level) in the two scenes with spheres
-    sunk into the r = 1000 ground.  Round 4's single-render comparison put
-    scene 12 at 0.21 level: the reference's own render-to-render noise there
-    is 0.097 level.  This test also found round 3's unclamped metal fuzz
-    above 1 (material.h:38): biases of up to -1.4 levels before the fix."""
+    below 1, spheres cut by the ground), against the reference's own noise:
+    its image means and segment counts from 24 independent streams (6 until
+    round 5; tests/golden/make_random_noise_golden.py runs oracle/_ref/
+    ref_harness, the reference's src/cpu) and 8 seeds of the kernel
+    algorithm.  Every channel's bias is within 0.1 level (a tenth of
+    north_star's 1/255) and 4 sigma of the two noises (round 6: worst 2.9
+    sigma), and every scene's segment count within 4 sigma -- except that in
+    the 8 scenes with a sphere cut by the ground the count may fall short by
+    up to 3e-3: there the reference traps more paths in the cavity between
+    the sphere and the ground, to the depth cap (measured and pinned by
+    test_ground_cut_sphere_segment_deficit_is_depth_capped_paths; DESIGN.md
+    4).  Round 4's single-render comparison put scene 12 at 0.21 level: the
+    reference's own render-to-render noise there is 0.097 level.  This test
+    also found round 3's unclamped metal fuzz above 1 (material.h:38):
+    biases of up to -1.4 levels before the fix."""
     import json
     import random_scenes
     with open(os.path.join(os.path.dirname(__file__), "golden", "ref_random_scenes_means.json")) as f:
         gold = json.load(f)
     w, spp = 96, 64
     cam = rtow.camera_cpu(aspect=16.0 / 9.0)
-    worst = worst_z = 0.0
+    worst = worst_z = worst_seg_z = 0.0
     for case in range(24):
         g = gold[str(case)]
         assert (g["width"], g["spp"], g["depth"]) == (w, spp, 50)
         ref = np.array(g["means"], np.float64)
+        rseg = np.array(g["segments"], np.float64)
+        assert len(ref) == len(rseg) == 24
         scene = random_scenes.free_scene(rtow, case)
         img, segs = [], []
         for seed in range(1, 9):
             sums, seg = kernel_render(scene, cam, rtow.make_params(w, int(w * 9 / 16), spp, seed=seed))
             img.append(rtow.tonemap(sums, spp).reshape(-1, 3).astype(np.float64).mean(0))
             segs.append(seg)
-        img = np.array(img)
+        img, segs = np.array(img), np.array(segs, np.float64)
         bias = img.mean(0) - ref.mean(0)
         sigma = np.sqrt(img.var(0, ddof=1) / len(img) + ref.var(0, ddof=1) / len(ref))
         worst = max(worst, float(np.abs(bias).max()))
         worst_z = max(worst_z, float(np.abs(bias / sigma).max()))
         assert np.abs(bias).max() <= 0.1, (case, bias)
-        assert np.abs(bias / sigma).max() <= 5.0, (case, bias, sigma)
-        assert abs(np.mean(segs) / np.mean(g["segments"]) - 1.0) <= 0.01, (case, segs, g["segments"])
-    print("worst bias %.4f level, worst %.2f sigma" % (worst, worst_z))
+        assert np.abs(bias / sigma).max() <= 4.0, (case, bias, sigma)
+        rel = segs.mean() / rseg.mean() - 1.0
+        z = (segs.mean() - rseg.mean()) / np.sqrt(segs.var(ddof=1) / len(segs) + rseg.var(ddof=1) / len(rseg))
+        if random_scenes.ground_cut_spheres(scene):
+            assert z <= 4.0 and rel >= -3e-3, (case, rel, z)
+        else:
+            worst_seg_z = max(worst_seg_z, abs(float(z)))
+            assert abs(z) <= 4.0, (case, rel, z)
+    print("worst bias %.4f level, worst %.2f sigma; segments (no ground-cut sphere) worst %.2f sigma"
+          % (worst, worst_z, worst_seg_z))
     assert worst > 0.0
+
+
+def test_ground_cut_sphere_segment_deficit_is_depth_capped_paths(rtow):
+    """Why the kernel algorithm traces up to ~1.5e-3 fewer segments than the
+    reference in scenes with spheres cut by the r = 1000 ground (VERDICT r5
+    item 2; DESIGN.md 4, "ground-cut spheres"): such a sphere and the ground
+    enclose a cavity (inside the ball, above the ground); a path that gets in
+    through the crease bounces there until the depth cap, 50 segments, and
+    returns black (src/cpu/main.cc:16-17).  The reference's fp64 arithmetic
+    lets more paths in than the fp32 specification.  Pinned on random scene
+    11 (8 ground-cut spheres) at 96x54x256 against the fp64 restatement of
+    src/cpu (byte-identical to the reference; depth-capped paths counted by
+    rto_reference_capped), with scene 15 (no ground-cut sphere) as control:
+      * scene 15: the kernel algorithm's depth-capped paths equal the
+        reference's within 3 Poisson sigma;
+      * scene 11: the kernel algorithm ends significantly fewer paths at the
+        cap (> 4 sigma; round 6: 975 vs 1 422 at 512 spp), 50 segments each,
+        and that accounts for the segment deficit (deficit < 50 x the
+        missing capped paths);
+      * RTO_OPT_FP64_HIT (the winner's root, hit point and normal in fp64)
+        moves the count halfway to the reference's: the fp32 hit point is
+        the mechanism.  The image is the same either way (capped paths are
+        black in both; test_kernel_algorithm_matches_reference_random_scenes)."""
+    import ctypes
+    import random_scenes
+    from oracle_lib import RTO_OPT_FP64_HIT, _kernel_render_opts, lib, reference_render_view
+    L = lib()
+    L.rto_reference_capped.restype = ctypes.c_ulonglong
+    L.rto_kernel_capped.restype = ctypes.c_ulonglong
+    L.rto_kernel_capped.argtypes = [ctypes.c_int]
+    w, h, spp = 96, 54, 256
+    cam = rtow.camera_cpu(aspect=16.0 / 9.0)
+    got = {}
+    for case in (11, 15):
+        scene = random_scenes.free_scene(rtow, case)
+        _, rseg = reference_render_view(scene, w, 16.0 / 9.0, spp)
+        rcap = L.rto_reference_capped()
+        row = {"ref": (rseg, rcap)}
+        for name, opt in (("spec", 0), ("fp64_hit", RTO_OPT_FP64_HIT)):
+            L.rto_kernel_capped(1)
+            seg = sum(_kernel_render_opts(scene, cam, rtow.make_params(w, h, spp, seed=s), opt, False, 0)[2]
+                      for s in (1, 2)) / 2.0
+            row[name] = (seg, L.rto_kernel_capped(1) / 2.0)
+        got[case] = row
+        print(case, row)
+    (rs, rc), (ks, kc), (_, hc) = got[15]["ref"], got[15]["spec"], got[15]["fp64_hit"]
+    assert abs(kc - rc) <= 3.0 * np.sqrt(rc + kc / 2.0), got[15]
+    (rs, rc), (ks, kc), (_, hc) = got[11]["ref"], got[11]["spec"], got[11]["fp64_hit"]
+    assert rc - kc > 4.0 * np.sqrt(rc + kc / 2.0), got[11]
+    assert 0.0 < rs - ks < 50.0 * (rc - kc), got[11]
+    assert kc < hc < rc, got[11]
 
 
 def test_kernel_algorithm_c0_bias_within_reference_stream_noise(rtow):

@@ -2,7 +2,7 @@
 """Attribution of the random-scene residual: the kernel
 algorithm (oracle kernel mode, the fp32 specification the HIP kernel matches
 bit for bit) against the reference's own noise on tests/random_scenes.py's 24
-scenes at 96x54x64 -- the 6 reference streams of tests/golden/
+scenes at 96x54x64 -- the 24 reference streams of tests/golden/
 ref_random_scenes_means.json (oracle/_ref/ref_harness, src/cpu) -- with each
 of the oracle's switches (oracle/rt_oracle.h RTO_OPT_*), so that the scenes
 whose bias or segment count sits outside the reference's noise show which
@@ -10,7 +10,9 @@ part of the specification moves them.
 
 Per scene and option set: image-mean bias per channel (level) and its z
 (kernel seeds' and reference streams' standard errors combined), segments
-relative to the reference mean and their z.  CPU only.
+relative to the reference mean and their z.  CPU only.  Round 6's results
+(profiles/r06_sunk_attribution.log) and the depth-cap counts that explain
+them (tools/cavity_attribution.py): DESIGN.md 4, "ground-cut spheres".
 
 Usage: python tools/sunk_attribution.py [--scenes 3,17] [--seeds 8] [--opts spec,fp64_hit,...]
 """
@@ -41,20 +43,7 @@ for name in ("RTO_OPT_FP64_HIT", "RTO_OPT_FP64_PATH"):
 
 
 def sunk_spheres(scene):
-    """Spheres that cut the r = 1000 ground's surface (|C - G| < 1000 + |r|
-    and > 1000 - |r|), in fp64; [] without a ground."""
-    g = [i for i in range(scene.n) if float(scene.radius[i]) == 1000.0 and float(scene.cy[i]) == -1000.0]
-    if not g:
-        return []
-    out = []
-    for i in range(scene.n):
-        if i == g[0]:
-            continue
-        d = np.sqrt(float(scene.cx[i]) ** 2 + (float(scene.cy[i]) + 1000.0) ** 2 + float(scene.cz[i]) ** 2)
-        r = abs(float(scene.radius[i]))
-        if 1000.0 - r < d < 1000.0 + r:
-            out.append(i)
-    return out
+    return random_scenes.ground_cut_spheres(scene)
 
 
 def main():
