@@ -30,23 +30,27 @@ def main():
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--preset", choices=["c2", "c4"], default="c2",
+                    help="c4: rank 0's 1/8 share of C4 (16384^2, 10 001 spheres, cells in LDS) at --spp")
     a = ap.parse_args()
     os.environ.setdefault("RTOW_LIB", os.path.join(ROOT, "build", "variants", "lanes.so"))
     import rtow
     L = rtow.lib()
     L.rt_lane_profile_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
     buf = (ctypes.c_ulonglong * (3 * len(REGIONS)))()
-    W, H = a.width, a.height
+    W, H = (a.width, a.height) if a.preset == "c2" else (16384, 16384)
+    world = 1 if a.preset == "c2" else 8
     cam = rtow.camera_cpu(aspect=W / H)
     flags = rtow.RT_FLAG_ACCEL_BVH | rtow.RT_FLAG_PILOT_SCHEDULE
     with rtow.Context(0) as ctx:
-        ctx.upload(rtow.final_scene())
-        ctx.render(cam, rtow.make_params(W, H, a.spp, seed=1, flags=flags))  # pilot + grid fit
+        ctx.upload(rtow.final_scene(half_extent=11 if a.preset == "c2" else 50))
+        ctx.render(cam, rtow.make_params(W, H, a.spp, seed=1, flags=flags, world=world))  # pilot + grid fit
         assert L.rt_lane_profile_read(buf, 1) == len(REGIONS)
-        _, st = ctx.render(cam, rtow.make_params(W, H, a.spp, seed=2, flags=flags))
+        _, st = ctx.render(cam, rtow.make_params(W, H, a.spp, seed=2, flags=flags, world=world))
         assert L.rt_lane_profile_read(buf, 1) == len(REGIONS)
     ws = st.wave_steps
-    out = {"workload": f"{W}x{H}x{a.spp} final scene, layer grid in LDS, pilot order",
+    out = {"workload": (f"{W}x{H}x{a.spp} final scene, layer grid in LDS, pilot order" if a.preset == "c2" else
+                        f"C4 rank 0 of 8: {W}x{H}x{a.spp}, 10 001 spheres, cells in LDS, pilot order"),
            "lib": os.path.relpath(rtow.LIB_PATH, ROOT), "segments": st.segments, "wave_steps": ws,
            "lane_efficiency": st.segments / (64.0 * ws), "regions": {}}
     print("%-13s %10s %9s %9s" % ("region", "per step", "exec", "useful"))
