@@ -47,6 +47,23 @@ def refs(scene):
     return np.stack(out)
 
 
+SCENES = ("final", "contact", "five", "embed", "negop", "hot")
+
+
+def scene_and_camera(rtow, name):
+    """The scene and camera ref_harness renders for `name`: the final scene and
+    the file: fixtures with the final scene's camera (13, 2, 3) -> 0, vfov 20,
+    aperture 0.1 (src/cpu/main.cc:90-97), the five-sphere scene with its own
+    (ref_harness.cc: (-2, 2, 1) -> (0, 0, -1), no lens, focus 3.4)."""
+    import fixture_scenes
+    if name == "final":
+        return rtow.final_scene(), rtow.camera_cpu(aspect=16.0 / 9.0)
+    if name == "five":
+        return rtow.five_scene(), rtow.camera_cpu(lookfrom=(-2, 2, 1), lookat=(0, 0, -1), aspect=16.0 / 9.0,
+                                                  aperture=0.0, focus_dist=3.4)
+    return fixture_scenes.FIXTURES[name](rtow), rtow.camera_cpu(aspect=16.0 / 9.0)
+
+
 def exceed(a, b):
     return float((np.abs(a.astype(np.int16) - b.astype(np.int16)) > 1).mean())
 

@@ -2,8 +2,10 @@
 """Converged per-pixel fixtures (north_star's "per-channel
 PPM delta <= 1/255 vs src/cpu", tested pixel by pixel): the REFERENCE itself
 (oracle/_ref/ref_harness, src/cpu built from /root/reference) renders the
-final scene and the contact fixture (tests/fixture_scenes.py) at 128x72,
-16 384 spp, depth 50, from 3 independent streams each.
+final scene, the five-sphere book scene (hollow glass, its own camera) and
+the contact / embed / negop / hot fixtures (tests/fixture_scenes.py) at
+128x72, 16 384 spp, depth 50, from 3 independent streams each (round 6:
+final and contact first, the other four added later with --scenes).
 
 Stream k discards SKIP = k * 4*10^9 random_double() draws after the scene is
 built (ref_harness.cc's SKIP); one 128x72x16384 render draws about 2.1*10^9,
@@ -31,7 +33,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
 W, ASPN, ASPD, DEPTH = 128, 16, 9, 50
 SKIP_STRIDE = 4_000_000_000
-SCENES = ("final", "contact")
+SCENES = ("final", "contact", "five", "embed", "negop", "hot")
 
 
 def name(scene, spp, k):
@@ -43,6 +45,7 @@ def main():
     ap.add_argument("--streams", type=int, default=3)
     ap.add_argument("--spp", type=int, default=16384)
     ap.add_argument("--jobs", type=int, default=6)
+    ap.add_argument("--scenes", default=",".join(SCENES))
     a = ap.parse_args()
     if not os.path.isdir("/root/reference"):
         sys.exit("make_converged_golden.py needs /root/reference (build container only)")
@@ -51,9 +54,11 @@ def main():
     import rtow
     import fixture_scenes
     from random_scenes import dump_scene_exact
-    contact = os.path.join(tempfile.mkdtemp(), "contact.txt")
-    dump_scene_exact(fixture_scenes.contact_scene(rtow), contact)
-    arg = {"final": "final", "contact": "file:" + contact}
+    arg = {"final": "final", "five": "five"}
+    for key in ("contact", "embed", "negop", "hot"):
+        path = os.path.join(tempfile.mkdtemp(), key + ".txt")
+        dump_scene_exact(fixture_scenes.FIXTURES[key](rtow), path)
+        arg[key] = "file:" + path
 
     def one(job):
         scene, k = job
@@ -68,11 +73,17 @@ def main():
         print(scene, k, st, flush=True)
         return scene, k, st
 
-    jobs = [(s, k) for s in SCENES for k in range(a.streams)]
+    jobs = [(s, k) for s in a.scenes.split(",") for k in range(a.streams)]
     with ThreadPoolExecutor(max_workers=a.jobs) as ex:
         res = list(ex.map(one, jobs))
+    meta = os.path.join(HERE, "ref_conv_streams.json")
     out = {"width": W, "height": W * ASPD // ASPN, "spp": a.spp, "depth": DEPTH, "skip_stride": SKIP_STRIDE,
            "scenes": {}}
+    if os.path.exists(meta):  # keep the scenes rendered before
+        with open(meta) as f:
+            old = json.load(f)
+        if (old["width"], old["spp"]) == (W, a.spp):
+            out["scenes"] = {k: v for k, v in old["scenes"].items() if k not in a.scenes.split(",")}
     for scene, k, st in sorted(res):
         e = out["scenes"].setdefault(scene, {"files": [], "segments": [], "seconds": []})
         e["files"].append(name(scene, a.spp, k))

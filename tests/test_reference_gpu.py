@@ -388,26 +388,26 @@ def test_rule_and_albedo_fixtures_vs_reference(rtow, gpu_ctx, key):
     fixture_scenes.p2_check(rtow, key, sums, segs)
 
 
-@pytest.mark.parametrize("scene_name", ["final", "contact"])
+@pytest.mark.parametrize("scene_name", ["final", "contact", "five", "embed", "negop", "hot"])
 def test_converged_per_pixel_vs_reference(rtow, gpu_ctx, scene_name):
     """north_star's "per-channel PPM delta <= 1/255 vs src/cpu", pixel by pixel
     (VERDICT r5 item 1): the product at 128x72, 16 384 spp, depth 50 (the
-    layer grid walk and the device write_color, 2 seeds) against the
-    reference's own converged renders (3 independent src/cpu streams,
-    tests/golden/make_converged_golden.py).  The fraction of channels more
-    than one level from a reference stream is at most max(1e-3, 1.5x) the
-    reference's own stream-to-stream fraction; no channel lies more than one
-    level from all of the other streams on one side more often than a
+    layer grid walk where the scene has a layer, and the device write_color;
+    2 seeds) against the reference's own converged renders (3 independent
+    src/cpu streams, tests/golden/make_converged_golden.py) of the final
+    scene, the contact fixture, the five-sphere book scene (a hollow glass
+    sphere) and the embed / negop / hot fixtures.  The fraction of channels
+    more than one level from a reference stream is at most max(1e-3, 1.5x)
+    the reference's own stream-to-stream fraction; no channel lies more than
+    one level from all of the other streams on one side more often than a
     reference stream does against its peers (tests/converged.py: no spatial
     cluster); image-mean bias within 0.05 level.  Measured: DESIGN.md 4."""
     import converged
-    import fixture_scenes
     R = converged.refs(scene_name)
     m = converged.meta()
     W, H, spp = m["width"], m["height"], m["spp"]
     assert R.shape == (3, H, W, 3)
-    scene = rtow.final_scene() if scene_name == "final" else fixture_scenes.contact_scene(rtow)
-    cam = rtow.camera_cpu(aspect=16.0 / 9.0)
+    scene, cam = converged.scene_and_camera(rtow, scene_name)
     gpu_ctx.upload(scene)
     for seed in (1, 2):
         sums, st = gpu_ctx.render(cam, rtow.make_params(W, H, spp, seed=seed, flags=GRID))
