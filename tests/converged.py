@@ -47,7 +47,13 @@ def refs(scene):
     return np.stack(out)
 
 
-SCENES = ("final", "contact", "five", "embed", "negop", "hot")
+SCENES = ("final", "contact", "five", "embed", "negop", "hot", "tenk")
+
+
+def size(name):
+    """(width, height, spp) of scene `name`'s converged fixture."""
+    m = meta()
+    return m["width"], m["height"], m["scenes"][name].get("spp", m["spp"])
 
 
 def scene_and_camera(rtow, name):
@@ -58,6 +64,8 @@ def scene_and_camera(rtow, name):
     import fixture_scenes
     if name == "final":
         return rtow.final_scene(), rtow.camera_cpu(aspect=16.0 / 9.0)
+    if name == "tenk":  # BASELINE C4's scene (10 001 spheres), the final scene's camera
+        return rtow.final_scene(half_extent=50), rtow.camera_cpu(aspect=16.0 / 9.0)
     if name == "five":
         return rtow.five_scene(), rtow.camera_cpu(lookfrom=(-2, 2, 1), lookat=(0, 0, -1), aspect=16.0 / 9.0,
                                                   aperture=0.0, focus_dist=3.4)

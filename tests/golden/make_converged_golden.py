@@ -17,7 +17,11 @@ Outputs (tests/golden/):
   ref_conv_<scene>_128x72x16384_s<k>.ppm.gz   k = 0, 1, 2
   ref_conv_streams.json                        segments / seconds per stream
 
-Usage: python tests/golden/make_converged_golden.py [--streams 3] [--spp 16384]
+The 10 001-sphere scene (BASELINE C4's, `tenk`; the reference scans every
+sphere per segment, ~20x the final scene's time) is rendered at 2048 spp:
+--scenes tenk --spp 2048.  Every scene records its spp.
+
+Usage: python tests/golden/make_converged_golden.py [--streams 3] [--spp 16384] [--scenes a,b]
 """
 import argparse
 import gzip
@@ -55,6 +59,9 @@ def main():
     import fixture_scenes
     from random_scenes import dump_scene_exact
     arg = {"final": "final", "five": "five"}
+    tenk = os.path.join(tempfile.mkdtemp(), "tenk.txt")
+    dump_scene_exact(rtow.final_scene(half_extent=50), tenk)
+    arg["tenk"] = "file:" + tenk
     for key in ("contact", "embed", "negop", "hot"):
         path = os.path.join(tempfile.mkdtemp(), key + ".txt")
         dump_scene_exact(fixture_scenes.FIXTURES[key](rtow), path)
@@ -77,15 +84,16 @@ def main():
     with ThreadPoolExecutor(max_workers=a.jobs) as ex:
         res = list(ex.map(one, jobs))
     meta = os.path.join(HERE, "ref_conv_streams.json")
-    out = {"width": W, "height": W * ASPD // ASPN, "spp": a.spp, "depth": DEPTH, "skip_stride": SKIP_STRIDE,
+    out = {"width": W, "height": W * ASPD // ASPN, "spp": 16384, "depth": DEPTH, "skip_stride": SKIP_STRIDE,
            "scenes": {}}
-    if os.path.exists(meta):  # keep the scenes rendered before
+    if os.path.exists(meta):  # keep the scenes rendered before (each records its spp)
         with open(meta) as f:
             old = json.load(f)
-        if (old["width"], old["spp"]) == (W, a.spp):
-            out["scenes"] = {k: v for k, v in old["scenes"].items() if k not in a.scenes.split(",")}
+        if old["width"] == W:
+            out["scenes"] = {k: dict(v, spp=v.get("spp", old["spp"])) for k, v in old["scenes"].items()
+                             if k not in a.scenes.split(",")}
     for scene, k, st in sorted(res):
-        e = out["scenes"].setdefault(scene, {"files": [], "segments": [], "seconds": []})
+        e = out["scenes"].setdefault(scene, {"spp": a.spp, "files": [], "segments": [], "seconds": []})
         e["files"].append(name(scene, a.spp, k))
         e["segments"].append(st["segments"])
         e["seconds"].append(round(st["seconds"], 1))

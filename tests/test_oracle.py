@@ -657,24 +657,24 @@ def test_tmin_in_ray_parameter_units_contact_fixture(rtow):
 
 
 
-@pytest.mark.parametrize("scene_name", ["contact", "five", "final"])
+@pytest.mark.parametrize("scene_name", ["contact", "five", "final", "tenk"])
 def test_converged_per_pixel_vs_reference(rtow, scene_name):
     """north_star's per-channel <= 1/255 bound, pixel by pixel, for the fp32
     kernel algorithm (the specification the HIP kernel matches bit for bit;
     VERDICT r5 item 1): at 128x72, 16 384 spp against the reference's 3
     converged src/cpu streams (tests/golden/make_converged_golden.py; bounds
     in tests/converged.py).  The contact fixture and the five-sphere scene
-    render whole (~10 s each on 8 cores); the final scene renders an 8-row
-    band through the frame's middle (rows 32-39: spheres, their contact
-    shadows and the horizon), the band a 9-way interleaved split of the frame
-    gives rank 4.  The GPU renders all six converged scenes whole
+    render whole (~10 s each on 8 cores); the final scene and BASELINE C4's
+    10 001-sphere scene (at 2048 spp: the reference scans every sphere) render
+    an 8-row band through the frame's middle (rows 32-39: spheres, their
+    contact shadows and the horizon), the band a 9-way interleaved split of
+    the frame gives rank 4.  The GPU renders all seven converged scenes whole
     (test_reference_gpu.py)."""
     import converged
     R = converged.refs(scene_name)
-    m = converged.meta()
-    W, H, spp = m["width"], m["height"], m["spp"]
+    W, H, spp = converged.size(scene_name)
     scene, cam = converged.scene_and_camera(rtow, scene_name)
-    if scene_name != "final":
+    if scene_name not in ("final", "tenk"):
         p, rows = rtow.make_params(W, H, spp, seed=1), None
     else:
         p = rtow.make_params(W, H, spp, seed=1, rank=4, world=9, row_block=8)

@@ -388,7 +388,7 @@ def test_rule_and_albedo_fixtures_vs_reference(rtow, gpu_ctx, key):
     fixture_scenes.p2_check(rtow, key, sums, segs)
 
 
-@pytest.mark.parametrize("scene_name", ["final", "contact", "five", "embed", "negop", "hot"])
+@pytest.mark.parametrize("scene_name", ["final", "contact", "five", "embed", "negop", "hot", "tenk"])
 def test_converged_per_pixel_vs_reference(rtow, gpu_ctx, scene_name):
     """north_star's "per-channel PPM delta <= 1/255 vs src/cpu", pixel by pixel
     (VERDICT r5 item 1): the product at 128x72, 16 384 spp, depth 50 (the
@@ -396,7 +396,8 @@ def test_converged_per_pixel_vs_reference(rtow, gpu_ctx, scene_name):
     2 seeds) against the reference's own converged renders (3 independent
     src/cpu streams, tests/golden/make_converged_golden.py) of the final
     scene, the contact fixture, the five-sphere book scene (a hollow glass
-    sphere) and the embed / negop / hot fixtures.  The fraction of channels
+    sphere), the embed / negop / hot fixtures and BASELINE C4's 10 001-sphere
+    scene (at 2048 spp: the grid's cells-in-LDS placement).  The fraction of channels
     more than one level from a reference stream is at most max(1e-3, 1.5x)
     the reference's own stream-to-stream fraction; no channel lies more than
     one level from all of the other streams on one side more often than a
@@ -404,8 +405,7 @@ def test_converged_per_pixel_vs_reference(rtow, gpu_ctx, scene_name):
     cluster); image-mean bias within 0.05 level.  Measured: DESIGN.md 4."""
     import converged
     R = converged.refs(scene_name)
-    m = converged.meta()
-    W, H, spp = m["width"], m["height"], m["spp"]
+    W, H, spp = converged.size(scene_name)
     assert R.shape == (3, H, W, 3)
     scene, cam = converged.scene_and_camera(rtow, scene_name)
     gpu_ctx.upload(scene)
